@@ -1,0 +1,279 @@
+"""Benchmark: RS(10+2) encode+decode GiB/s, device-resident, 1 MiB objects.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload encdec|enc|dec4]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+A step = one pass of the hot path over one batch: encode the batch (parity
+rows <- M x data rows, Client.encode / ecRedis.go:390) then decode it
+(reconstruct data shards {0, 5} from the first 10 present shards, the fused
+Client.decode / ecRedis.go:406-420 with the proxy's first-d rule: exactly k
+shards arrive).  Each rank owns its own batch of 1024 objects (object-per-
+rank, weak scaling); RCCL all_reduce of one int is the start/finish barrier.
+value = object bytes x ops of all ranks / max-over-ranks time.
+
+Prints ONE JSON line (rank 0) with roofline (HIP-event kernel timing, the
+committed rocprofv3 PMC traffic when available) and cpu_baseline (the
+oracle's AVX2 port of the Go path, timed on this host, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # name: (k, p, object bytes, batch per GPU, erased rows for decode, ops)
+    "encdec": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(0, 5), ops=("encode", "decode"),
+                   desc="RS(10+2) encode+decode, 1 MiB objects, batch 1024/GPU, device-resident"),
+    "enc": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(), ops=("encode",),
+                desc="RS(10+2) encode, 1 MiB objects, batch 1024/GPU, device-resident"),
+    "dec4": dict(k=10, p=4, nbytes=4 << 20, batch=512, lost=(0, 5), ops=("decode",),
+                 desc="RS(10+4) decode, 2 missing data shards {0,5}, 4 MiB objects, batch 512/GPU"),
+}
+METRICS = {
+    "encdec": "RS(10+2) encode+decode GiB/s (device-resident), 1 MB objects, 1/2/4/8 GPU",
+    "enc": "RS(10+2) encode GiB/s (device-resident), 1 MB objects",
+    "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(w, sample_objs, enc_matrix, inv_rows, gpu_sample, budget_s=10.0, threads=16):
+    """Time the oracle's AVX2 port of the Go path (galMulAVX2Xor +
+    codeSomeShardsP, maxGoroutines 32, minSplitSize 1024) on `threads` host
+    threads over a bounded sample, and bit-compare it with the GPU output."""
+    import oracle
+    k, p = w["k"], w["p"]
+    S = (w["nbytes"] + k - 1) // k
+    n = k + p
+    lost = list(w["lost"])
+    surv = [i for i in range(n) if i not in lost][:k]
+    objs = sample_objs  # list of (n, S) uint8 arrays, data rows filled
+    done_bytes, t0, reps = 0, time.perf_counter(), 0
+    while True:
+        for o in objs:
+            if "encode" in w["ops"]:
+                par = oracle.code_fast(enc_matrix[k:], [o[c] for c in range(k)], nthreads=threads,
+                                       max_goroutines=32)
+                for r in range(p):
+                    o[k + r] = par[r]
+            if "decode" in w["ops"]:
+                rec = oracle.code_fast(inv_rows, [o[c] for c in surv], nthreads=threads,
+                                       max_goroutines=32)
+                for j, i in enumerate(lost):
+                    o[i] = rec[j]
+            done_bytes += w["nbytes"] * len(w["ops"])
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    exact = all(np.array_equal(objs[i], gpu_sample[i]) for i in range(len(objs)))
+    return {
+        "value": round(done_bytes / el / GiB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{len(objs)} x {w['nbytes'] >> 20} MiB objects x {reps} reps "
+                  f"({' + '.join(w['ops'])}), {el:.1f} s; oracle/rs_oracle.c AVX2 PSHUFB + "
+                  f"codeSomeShardsP split on {threads} threads (Go toolchain/module unavailable "
+                  f"offline); bit-exact vs GPU: {exact}",
+    }
+
+
+def pmc_traffic(kernel_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (separate
+    --pmc passes; gfx950 FETCH_SIZE x2 correction, MI355X_MICROARCH.md §HBM)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return d["kernels"][kernel_key]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="objects per GPU (default: workload's)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import infinicache_amd as ia
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if not ia.device_ok(local):
+        raise SystemExit(f"rank {rank}: no usable gfx950 device at cuda:{local}")
+
+    w = WORKLOADS[args.workload]
+    k, p = w["k"], w["p"]
+    n = k + p
+    nobj = args.batch or w["batch"]
+    S = (w["nbytes"] + k - 1) // k
+    pitch = (S + 255) // 256 * 256
+    stride = n * pitch
+    enc = ia.New(k, p, device=local)
+    stream = torch.cuda.current_stream(dev)
+
+    # synthetic objects: uniform random bytes, generated on device per rank
+    g = torch.Generator(device=dev).manual_seed(0x1F1C + rank)
+    buf = torch.randint(0, 256, (nobj, n, pitch), dtype=torch.uint8, device=dev, generator=g)
+    buf[:, :, S:] = 0
+    bad = torch.zeros(nobj, dtype=torch.int32, device=dev)
+    present = [i not in w["lost"] for i in range(n)]
+    if "encode" not in w["ops"]:  # decode-only workload: start from valid parity
+        enc.encode_dev(buf, S, pitch, stride, nobj, stream)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        if "encode" in w["ops"]:
+            enc.encode_dev(buf, S, pitch, stride, nobj, stream)
+        if evs is not None:
+            evs[1].record(stream)
+        if "decode" in w["ops"]:
+            enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, stream)
+        if evs is not None:
+            evs[2].record(stream)
+
+    def barrier():
+        if world > 1:
+            t = torch.ones(1, dtype=torch.int32, device=dev)
+            dist.all_reduce(t)  # RCCL over xGMI: the only collective
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if int(bad.sum()) != 0:
+        raise SystemExit("decode reported a verify mismatch on synthetic data")
+
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    ops = len(w["ops"])
+    total_obj_bytes = world * nobj * w["nbytes"] * ops * args.steps
+    value = total_obj_bytes / elapsed / GiB
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # algorithmic bytes per launch: encode k*S read + p*S write;
+    # decode (e missing data rows) k*S read + e*S write; on unpadded S
+    e_rows = len(w["lost"])
+    enc_bytes = nobj * (k + p) * S
+    dec_bytes = nobj * (k + e_rows) * S
+    per_kernel = {}
+    if "encode" in w["ops"]:
+        per_kernel["encode"] = (enc_bytes, enc_ms)
+    if "decode" in w["ops"]:
+        per_kernel["decode"] = (dec_bytes, dec_ms)
+    dom = max(per_kernel, key=lambda x: per_kernel[x][1])
+    dom_bytes, dom_ms = per_kernel[dom]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    kernel_key = f"gf_apply_kernel<{k},{p if dom == 'encode' else e_rows}>"
+    traffic = pmc_traffic(kernel_key)
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "kernel": f"{kernel_key} ({dom}), {dom_bytes} algorithmic B/launch, "
+                  f"{dom_ms * 1e3:.1f} us avg (HIP events)",
+        "per_kernel_GBps": {kk: round(b / (ms * 1e-3) / 1e9, 1) for kk, (b, ms) in per_kernel.items()},
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import rs_numpy as rn
+        ns = 8
+        sample_gpu = buf[:ns, :, :S].cpu().numpy()  # final GPU state of 8 objects
+        sample = [sample_gpu[i].copy() for i in range(ns)]
+        for o in sample:
+            if "encode" in w["ops"]:
+                o[k:] = 0          # CPU recomputes parity from the same data rows
+            else:
+                for i in w["lost"]:
+                    o[i] = 0       # CPU reconstructs the erased rows
+        m = enc.matrix()
+        surv = [i for i in range(n) if i not in w["lost"]][:k]
+        inv_rows = rn.invert(m[surv])[list(w["lost"])] if w["lost"] else None
+        cpu = cpu_baseline(w, sample, m, inv_rows, sample_gpu, budget_s=args.cpu_seconds,
+                           threads=int(os.environ.get("BENCH_CPU_THREADS", "16")))
+
+    if rank == 0:
+        out = {
+            "metric": METRICS[args.workload],
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: uniform random bytes (torch.randint on device, seeded per rank)",
+            "config": {
+                "workload": w["desc"],
+                "k": k, "p": p,
+                "object_bytes": w["nbytes"],
+                "shard_len": S,
+                "pitch": pitch,
+                "batch_per_gpu": nobj,
+                "decode_erasures": list(w["lost"]),
+                "parallelism": f"object-per-rank x{world} (RCCL all_reduce barrier only)",
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+/*
+ * rsgpu.h — C ABI of the MI355X-native Reed-Solomon (GF(2^8)) codec that
+ * replaces the InfiniCache client's erasure-coding hot path.
+ *
+ * Interface being replaced: the Go interface reedsolomon.Encoder
+ * (github.com/klauspost/reedsolomon v1.9.3, /root/reference/go.mod:16) held in
+ * Client.EC (/root/reference/client/client.go:38), built by NewEncoder
+ * (/root/reference/client/ec.go:14-24) and called from exactly
+ * /root/reference/client/ecRedis.go:384 (Split), :390 (Encode), :395/:406/:420
+ * (Verify), :415 (Reconstruct), :430 (Join).  The 7-method contract is mirrored
+ * by DummyEncoder at /root/reference/client/ec.go:30-121.
+ *
+ * Split/Join are host slicing and stay on the caller's side (Go shim / the
+ * Python host mirror in infinicache_amd/ec.py); every byte of GF arithmetic
+ * goes through the functions below onto hand-written HIP kernels for gfx950.
+ * There is no CPU compute fallback: without a usable device every compute
+ * entry point returns RSGPU_ERR_NO_DEVICE (argument validation, which follows
+ * the upstream error precedence, still runs first).
+ *
+ * Conventions
+ *   - return 0 on success, a negative RSGPU_ERR_* code otherwise;
+ *   - shard "present" == non-zero length (Go: len(shard) != 0; nil == empty);
+ *   - the library never retains a caller pointer after a call returns; host
+ *     calls are synchronous (all device work done, outputs written);
+ *   - contexts are safe for concurrent use from several threads.
+ */
+#ifndef RSGPU_H
+#define RSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes: 1:1 onto the upstream Go error values ---------------- */
+#define RSGPU_OK 0
+#define RSGPU_ERR_INV_SHARD_NUM -1        /* reedsolomon.ErrInvShardNum      */
+#define RSGPU_ERR_MAX_SHARD_NUM -2        /* reedsolomon.ErrMaxShardNum      */
+#define RSGPU_ERR_TOO_FEW_SHARDS -3       /* reedsolomon.ErrTooFewShards     */
+#define RSGPU_ERR_SHARD_NO_DATA -4        /* reedsolomon.ErrShardNoData      */
+#define RSGPU_ERR_SHARD_SIZE -5           /* reedsolomon.ErrShardSize        */
+#define RSGPU_ERR_SINGULAR -6             /* reedsolomon errSingular         */
+#define RSGPU_ERR_SHORT_DATA -7           /* reedsolomon.ErrShortData        */
+#define RSGPU_ERR_RECONSTRUCT_REQUIRED -8 /* reedsolomon.ErrReconstructRequired */
+#define RSGPU_ERR_INVALID_INPUT -9        /* reedsolomon.ErrInvalidInput     */
+#define RSGPU_ERR_NOT_IMPLEMENTED -10     /* client.ErrNotImplemented (ec.go:10-12) */
+/* library-level failures (no Go counterpart) */
+#define RSGPU_ERR_INVALID_ARG -20         /* NULL pointer, bad layout/alignment */
+#define RSGPU_ERR_NO_DEVICE -21           /* no HIP device / device id out of range */
+#define RSGPU_ERR_HIP -22                 /* a HIP runtime call failed */
+#define RSGPU_ERR_NOMEM -23               /* host or device allocation failed */
+
+/* ---- rsgpu_create flags ------------------------------------------------ */
+#define RSGPU_MATRIX_VANDERMONDE 0u /* default: upstream buildMatrix          */
+#define RSGPU_MATRIX_CAUCHY 1u      /* upstream WithCauchyMatrix()            */
+#define RSGPU_MATRIX_PAR1 2u        /* upstream WithPAR1Matrix()              */
+#define RSGPU_MATRIX_MASK 3u
+
+typedef struct rsgpu_ctx rsgpu_ctx;
+
+/* Replaces reedsolomon.New(dataShards, parityShards, opts...) as called at
+ * /root/reference/client/ec.go:19.  Rejects data<=0 || parity<=0
+ * (RSGPU_ERR_INV_SHARD_NUM) and data+parity > 256 (RSGPU_ERR_MAX_SHARD_NUM).
+ * Builds the coding matrix on the host; device resources are created lazily
+ * on the first compute call on `device`.  *out is NULL on error. */
+int rsgpu_create(int data_shards, int parity_shards, int device, unsigned flags, rsgpu_ctx **out);
+void rsgpu_destroy(rsgpu_ctx *ctx);
+
+int rsgpu_data_shards(const rsgpu_ctx *ctx);
+int rsgpu_parity_shards(const rsgpu_ctx *ctx);
+/* Copies the (data+parity) x data coding matrix, row-major, into out. */
+int rsgpu_matrix(const rsgpu_ctx *ctx, uint8_t *out);
+const char *rsgpu_strerror(int code);
+/* Number of visible HIP devices (0 when none); never fails. */
+int rsgpu_device_count(void);
+/* 1 if the library's gfx950 code object can run on `device`, else 0. */
+int rsgpu_device_ok(int device);
+
+/* ---- per-object host-memory API (what the Go shim forwards to) ---------- */
+/* shards[i]: caller-owned host buffer of lens[i] bytes; lens[i] == 0 marks a
+ * nil/empty shard.  nshards must equal data+parity (else TOO_FEW_SHARDS). */
+
+/* Encode (upstream Encode; ecRedis.go:390): checkShards(nilok=false), then
+ * shards[k..k+p) = parity.  All shards must be allocated (len == size). */
+int rsgpu_encode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards);
+
+/* Verify (upstream Verify; ecRedis.go:395,406,420): *ok = 1 iff every parity
+ * shard equals the parity recomputed from the data shards.  Any nil shard ->
+ * (*ok = 0, RSGPU_ERR_SHARD_SIZE) with no device work, as upstream. */
+int rsgpu_verify(rsgpu_ctx *ctx, const uint8_t *const *shards, const size_t *lens, int nshards,
+                 int *ok);
+
+/* Reconstruct / ReconstructData (upstream reconstruct(shards, dataOnly);
+ * ecRedis.go:415).  lens[i] == 0 marks shard i missing; for every missing
+ * shard the caller passes a writable buffer of the common shard size in
+ * shards[i] (upstream re-uses cap >= size, else allocates — the Go shim does
+ * that allocation before the call).  Survivors are the first `data` present
+ * shards in index order; inverses are cached per erasure pattern (upstream
+ * inversionTree).  data_only = 1 leaves missing parity shards untouched. */
+int rsgpu_reconstruct(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
+                      int data_only);
+
+/* Fused Client.decode (ecRedis.go:404-427: Reconstruct, then Verify) in ONE
+ * device pass: reconstructs every missing shard in place and sets *ok to the
+ * result the upstream Verify-after-Reconstruct would return.  Returns
+ * without device work (ok = 1) when nothing is missing and verify passes. */
+int rsgpu_decode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards, int *ok);
+
+/* Update (upstream Update): for each non-nil newdata[c] (new_lens[c] != 0):
+ * shards[c] ^= newdata[c] (the old buffer becomes the delta, as upstream) and
+ * parity ^= M[.,c] * delta.  nnew must equal data. */
+int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
+                 const uint8_t *const *newdata, const size_t *new_lens, int nnew);
+
+/* ---- batched device-resident API (HBM in, HBM out) ---------------------
+ * Layout: shard i of object o lives at d_base + o*obj_stride + i*pitch, for
+ * i in [0, data+parity).  Requirements: d_base and obj_stride 16-B aligned,
+ * pitch % 16 == 0, pitch >= shard_len rounded up to 16, and
+ * (data+parity-1)*pitch + pitch < 4 GiB.  Kernels read/write whole 16-B
+ * vectors, so written rows' bytes in [shard_len, roundup16(shard_len)) are
+ * overwritten with the coding of the input rows' pad bytes (zero when those
+ * are zero).  `stream` is a hipStream_t (NULL = default stream); calls are
+ * asynchronous on it and make no host<->device synchronisation. */
+
+/* Encode nobj objects: rows [k, k+p) <- M[k:] x rows [0, k). */
+int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitch,
+                     size_t obj_stride, int nobj, void *stream);
+
+/* Verify nobj objects: d_bad[o] (device, uint32) is set to 1 when object o's
+ * parity mismatches, 0 otherwise. */
+int rsgpu_verify_dev(rsgpu_ctx *ctx, const void *d_base, size_t shard_len, size_t pitch,
+                     size_t obj_stride, int nobj, uint32_t *d_bad, void *stream);
+
+/* Reconstruct nobj objects sharing one erasure pattern: present[i] (host,
+ * data+parity bytes) != 0 marks row i present; missing rows are written in
+ * place (parity rows too unless data_only). */
+int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                          size_t pitch, size_t obj_stride, int nobj, int data_only, void *stream);
+
+/* Fused decode (Reconstruct + Verify) of nobj objects sharing one pattern;
+ * d_bad[o] = 1 when upstream's Verify-after-Reconstruct would fail for o. */
+int rsgpu_decode_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                     size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSGPU_H */

@@ -1,0 +1,14 @@
+"""infinicache_amd — MI355X-native Reed-Solomon erasure coding for the
+InfiniCache client (drop-in for reedsolomon.Encoder under
+/root/reference/client/ec.go).  See DESIGN.md."""
+from .ec import (DummyEncoder, ErrInvalidInput, ErrInvShardNum, ErrMaxShardNum,  # noqa: F401
+                 ErrNotImplemented, ErrReconstructRequired, ErrShardNoData, ErrShardSize,
+                 ErrShortData, ErrSingular, ErrTooFewShards, HipError, InvalidArgument, New,
+                 NewEncoder, NoDevice, RSEncoder, RSError, device_count, device_ok)
+
+__all__ = [
+    "New", "NewEncoder", "RSEncoder", "DummyEncoder", "RSError", "device_count", "device_ok",
+    "ErrInvShardNum", "ErrMaxShardNum", "ErrTooFewShards", "ErrShardNoData", "ErrShardSize",
+    "ErrSingular", "ErrShortData", "ErrReconstructRequired", "ErrInvalidInput",
+    "ErrNotImplemented", "InvalidArgument", "NoDevice", "HipError",
+]

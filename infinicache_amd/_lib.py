@@ -1,0 +1,70 @@
+"""ctypes binding of librsgpu.so (the C ABI declared in include/rsgpu.h).
+
+The shared library is built in-tree by infinicache_amd/csrc/Makefile (see
+__graft_entry__.build()).  There is deliberately no fallback: if the library
+is missing, importing the codec raises, and every compute call on a machine
+without a gfx950 device returns RSGPU_ERR_NO_DEVICE.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librsgpu.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "rsgpu.h")
+
+# the exported entry points (kept in sync with include/rsgpu.h; tests check)
+EXPORTS = (
+    "rsgpu_create", "rsgpu_destroy", "rsgpu_data_shards", "rsgpu_parity_shards", "rsgpu_matrix",
+    "rsgpu_strerror", "rsgpu_device_count", "rsgpu_device_ok", "rsgpu_encode", "rsgpu_verify",
+    "rsgpu_reconstruct", "rsgpu_decode", "rsgpu_update", "rsgpu_encode_dev", "rsgpu_verify_dev",
+    "rsgpu_reconstruct_dev", "rsgpu_decode_dev",
+)
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u8pp = ctypes.POINTER(u8p)
+szp = ctypes.POINTER(ctypes.c_size_t)
+intp = ctypes.POINTER(ctypes.c_int)
+vp = ctypes.c_void_p
+sz = ctypes.c_size_t
+ci = ctypes.c_int
+
+_lib = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load librsgpu.so; raise LibraryMissing (loudly) if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LibraryMissing(
+            f"{LIB_PATH} not found: build it with `make -C infinicache_amd/csrc` "
+            "(or python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(LIB_PATH)
+    L.rsgpu_create.argtypes = [ci, ci, ci, ctypes.c_uint, ctypes.POINTER(vp)]
+    L.rsgpu_destroy.argtypes = [vp]
+    L.rsgpu_destroy.restype = None
+    L.rsgpu_data_shards.argtypes = [vp]
+    L.rsgpu_parity_shards.argtypes = [vp]
+    L.rsgpu_matrix.argtypes = [vp, u8p]
+    L.rsgpu_strerror.argtypes = [ci]
+    L.rsgpu_strerror.restype = ctypes.c_char_p
+    L.rsgpu_device_count.argtypes = []
+    L.rsgpu_device_ok.argtypes = [ci]
+    L.rsgpu_encode.argtypes = [vp, u8pp, szp, ci]
+    L.rsgpu_verify.argtypes = [vp, u8pp, szp, ci, intp]
+    L.rsgpu_reconstruct.argtypes = [vp, u8pp, szp, ci, ci]
+    L.rsgpu_decode.argtypes = [vp, u8pp, szp, ci, intp]
+    L.rsgpu_update.argtypes = [vp, u8pp, szp, ci, u8pp, szp, ci]
+    L.rsgpu_encode_dev.argtypes = [vp, vp, sz, sz, sz, ci, vp]
+    L.rsgpu_verify_dev.argtypes = [vp, vp, sz, sz, sz, ci, vp, vp]
+    L.rsgpu_reconstruct_dev.argtypes = [vp, vp, u8p, sz, sz, sz, ci, ci, vp]
+    L.rsgpu_decode_dev.argtypes = [vp, vp, u8p, sz, sz, sz, ci, vp, vp]
+    _lib = L
+    return L

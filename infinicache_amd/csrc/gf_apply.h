@@ -1,0 +1,61 @@
+// gf_apply.h — host-side description of one GF(2^8) "coding-matrix x shards"
+// pass, and the launcher that runs it on gfx950.
+//
+// Every codec operation of reedsolomon.Encoder (Encode, Verify, Reconstruct,
+// ReconstructData, Update, and the fused Client.decode) is ONE linear map over
+// GF(2^8) from K input rows of an object to R output rows:
+//     out[r] = XOR_c coef[r][c] (x) in[c]
+// Rows [0, nw) are written to HBM; rows [nw, R) are "check rows" whose value
+// must be all-zero (a parity comparison folded into the matrix) and only set
+// a per-object mismatch flag.  The host derives coef from the coding matrix
+// (upstream buildMatrix / cached inverses); the kernel never branches on the
+// operation.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+
+namespace rsgpu {
+
+// Kernel coefficient format: a coefficient c is stored as four u32 lookup
+// tables, one per 2-bit group g of the input byte: byte j of tab[g] is
+// c (x) (j << 2g).  Because multiplication by c is GF(2)-linear,
+// c (x) x = XOR_g tab[g][(x >> 2g) & 3], which v_perm_b32 evaluates for four
+// bytes at once.
+void coef_tables(uint8_t c, uint32_t out[4]);
+
+struct Plan {
+    int K = 0;                   // inputs
+    int R = 0;                   // outputs
+    int nw = 0;                  // rows [0, nw) written, [nw, R) checked
+    std::vector<int> in_rows;    // K row indices within an object
+    std::vector<int> out_rows;   // R row indices (checked rows: unused)
+    std::vector<uint8_t> coef;   // R x K
+    std::vector<uint32_t> tab;   // [R][K][4] kernel tables
+    // device copies for the generic (K > 16) kernel; uploaded once, then
+    // immutable (safe for concurrent launches)
+    uint32_t *d_tab = nullptr;     // [K][R][4] (input-major)
+    uint32_t *d_in_row = nullptr;  // [K]
+    std::once_flag dev_once;
+    hipError_t dev_err = hipSuccess;
+    void build_tables();
+    ~Plan();
+};
+
+struct Layout {
+    uint8_t *base;        // object 0
+    size_t obj_stride;    // bytes between objects
+    size_t pitch;         // bytes between rows of an object
+    size_t shard_len;     // bytes per shard (S)
+    int nobj;
+};
+
+// Launches the plan over all objects on `stream`.  d_bad (nobj u32) must be
+// zeroed by the caller when the plan has check rows.  Returns hipSuccess or
+// the first HIP error.
+hipError_t launch_plan(Plan &plan, const Layout &L, uint32_t *d_bad, hipStream_t stream);
+
+}  // namespace rsgpu

@@ -1,0 +1,346 @@
+// gf_kernels.hip — the hot path: GF(2^8) coding-matrix x object-shard kernels
+// for CDNA4 (gfx950).  Replaces the upstream galMulSlice/galMulSliceXor SIMD
+// loops and codeSomeShards(P) byte-range goroutine split that sit under
+// reedsolomon.Encoder.Encode/Verify/Reconstruct (called from
+// /root/reference/client/ecRedis.go:390,395,406,415,420).
+//
+// Design:
+//   * one workgroup = 256 lanes x 16 B of one object; grid.y = object;
+//   * every input row is read once with buffer_load_dwordx4 (1 KiB per wave
+//     instruction, the object base in a uniform SRD, the row offset in
+//     soffset => no per-row VALU address math);
+//   * all R outputs accumulate in VGPRs; GF multiply-by-constant is four
+//     v_perm_b32 byte lookups on 2-bit groups of the input (tables in SGPRs,
+//     from the kernarg segment) merged with v_bitop3 (3-input XOR, gfx950);
+//   * rows [0, nw) are stored with buffer_store_dwordx4; rows [nw, R) are
+//     compare-to-zero rows that raise a per-object flag (fused Verify).
+// No MFMA and no LDS: the op is HBM-bound byte arithmetic.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "gf_apply.h"
+#include "gf256.h"
+
+namespace rsgpu {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;
+constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
+constexpr int kMaxR = 4;   // and up to 4 output rows per pass
+
+void coef_tables(uint8_t c, uint32_t out[4]) {
+    const GF &g = gf();
+    for (int grp = 0; grp < 4; ++grp) {
+        uint32_t w = 0;
+        for (int j = 0; j < 4; ++j) w |= (uint32_t)g.mul(c, (uint8_t)(j << (2 * grp))) << (8 * j);
+        out[grp] = w;
+    }
+}
+
+void Plan::build_tables() {
+    tab.assign((size_t)R * K * 4, 0);
+    for (int r = 0; r < R; ++r)
+        for (int c = 0; c < K; ++c) coef_tables(coef[(size_t)r * K + c], &tab[((size_t)r * K + c) * 4]);
+}
+
+Plan::~Plan() {
+    if (d_tab) (void)hipFree(d_tab);
+    if (d_in_row) (void)hipFree(d_in_row);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t lut(uint32_t t, uint32_t sel) {
+    return __builtin_amdgcn_perm(t, t, sel);
+}
+
+// acc ^= c (x) w, for one dword w whose 2-bit group indices are i0..i3.
+__device__ __forceinline__ uint32_t gf_mac(uint32_t acc, const uint32_t *t, uint32_t i0,
+                                           uint32_t i1, uint32_t i2, uint32_t i3) {
+    acc = xor3(acc, lut(t[0], i0), lut(t[1], i1));
+    return xor3(acc, lut(t[2], i2), lut(t[3], i3));
+}
+
+// mask of the valid bytes of dword d in a 16-B vector holding `valid` bytes
+__device__ __forceinline__ uint32_t tail_mask(int d, uint32_t valid) {
+    int v = (int)valid - 4 * d;
+    if (v >= 4) return 0xffffffffu;
+    if (v <= 0) return 0u;
+    return (1u << (8 * v)) - 1u;
+}
+
+template <int K, int R>
+struct ApplyArgs {
+    const uint8_t *base;
+    uint64_t obj_stride;
+    uint32_t *bad;
+    uint32_t nvec;  // 16-B vectors per row
+    uint32_t tail;  // valid bytes in the last vector (1..16)
+    uint32_t nw;
+    uint32_t span;  // bytes addressable from an object base
+    uint32_t in_off[K];
+    uint32_t out_off[R];
+    uint32_t tab[K * R * 4];  // input-major [K][R][4]: one s_load_dwordx(4R) per input
+};
+
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_kernel(const ApplyArgs<K, R> a) {
+    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    if (v >= a.nvec) return;
+    const uint8_t *ob = a.base + (uint64_t)blockIdx.y * a.obj_stride;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
+    const uint32_t voff = v * 16u;
+
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_off[c], 0);
+
+    uint32_t acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t w = x[c][d];
+            const uint32_t i0 = w & 0x03030303u;
+            const uint32_t i1 = (w >> 2) & 0x03030303u;
+            const uint32_t i2 = (w >> 4) & 0x03030303u;
+            const uint32_t i3 = (w >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], &a.tab[(c * R + r) * 4], i0, i1, i2, i3);
+        }
+        // keep the input-at-a-time order: without these fences the IR
+        // passes and the scheduler hoist every input's index math and split
+        // the work row by row (160+ VGPRs, 2 waves/SIMD)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    bool mismatch = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if ((uint32_t)r < a.nw) {
+            u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+            __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, a.out_off[r], 0);
+        } else {
+            const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+        }
+    }
+    if (mismatch) atomicOr(a.bad + blockIdx.y, 1u);
+}
+
+// Generic pass for K > 16 inputs (any shard count up to 256): runtime input
+// loop, tables read by scalar loads from a device buffer laid out [K][R][4].
+struct GenericArgs {
+    const uint8_t *base;
+    uint64_t obj_stride;
+    uint32_t *bad;
+    const uint32_t *tab;     // [K][rstride][4], pre-offset to this pass's first row
+    const uint32_t *in_row;  // [K] row indices; offset = row * pitch
+    uint32_t nvec, tail, nw, span, K, rstride, pitch;
+    uint32_t out_off[kMaxR];
+};
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) {
+    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    if (v >= a.nvec) return;
+    const uint8_t *ob = a.base + (uint64_t)blockIdx.y * a.obj_stride;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
+    const uint32_t voff = v * 16u;
+    uint32_t acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+    for (uint32_t c = 0; c < a.K; ++c) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_row[c] * a.pitch, 0);
+        const uint32_t *t = a.tab + (size_t)c * a.rstride * 4;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t w = x[d];
+            const uint32_t i0 = w & 0x03030303u;
+            const uint32_t i1 = (w >> 2) & 0x03030303u;
+            const uint32_t i2 = (w >> 4) & 0x03030303u;
+            const uint32_t i3 = (w >> 6) & 0x03030303u;
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], t + r * 4, i0, i1, i2, i3);
+        }
+    }
+    bool mismatch = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if ((uint32_t)r < a.nw) {
+            u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+            __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, a.out_off[r], 0);
+        } else {
+            const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+        }
+    }
+    if (mismatch) atomicOr(a.bad + blockIdx.y, 1u);
+}
+
+// ----------------------------------------------------------------- launchers
+
+namespace {
+
+constexpr int kMaxGridY = 65535;
+
+struct Sub {  // one pass over <= kMaxR output rows of a plan
+    int r0, R, nw;
+};
+
+template <int K, int R>
+hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
+                        hipStream_t st) {
+    ApplyArgs<K, R> a;
+    a.obj_stride = L.obj_stride;
+    a.nvec = (uint32_t)((L.shard_len + 15) / 16);
+    a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
+    a.nw = (uint32_t)s.nw;
+    int maxrow = 0;
+    for (int c = 0; c < K; ++c) {
+        a.in_off[c] = (uint32_t)(p.in_rows[c] * L.pitch);
+        maxrow = std::max(maxrow, p.in_rows[c]);
+    }
+    for (int r = 0; r < R; ++r) {
+        const int row = p.out_rows[s.r0 + r];
+        a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * L.pitch);
+        maxrow = std::max(maxrow, row);
+        for (int c = 0; c < K; ++c)
+            for (int g = 0; g < 4; ++g)
+                a.tab[(c * R + r) * 4 + g] = p.tab[((size_t)(s.r0 + r) * K + c) * 4 + g];
+    }
+    a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * 16);
+    const unsigned gx = (a.nvec + kBlock - 1) / kBlock;
+    for (int o0 = 0; o0 < L.nobj; o0 += kMaxGridY) {
+        const int no = std::min(kMaxGridY, L.nobj - o0);
+        a.base = L.base + (size_t)o0 * L.obj_stride;
+        a.bad = d_bad ? d_bad + o0 : nullptr;
+        hipLaunchKernelGGL((gf_apply_kernel<K, R>), dim3(gx, no), dim3(kBlock), 0, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+template <int R>
+hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
+                          hipStream_t st) {
+    const int K = p.K;
+    // upload the [K][R][4] table image and row indices once per plan
+    hipError_t e = hipSuccess;
+    std::call_once(p.dev_once, [&] {
+        std::vector<uint32_t> t((size_t)K * p.R * 4), rows(K);
+        for (int c = 0; c < K; ++c) {
+            rows[c] = (uint32_t)p.in_rows[c];
+            for (int r = 0; r < p.R; ++r)
+                for (int g = 0; g < 4; ++g)
+                    t[((size_t)c * p.R + r) * 4 + g] = p.tab[((size_t)r * K + c) * 4 + g];
+        }
+        e = hipMalloc(&p.d_tab, t.size() * 4);
+        if (e == hipSuccess) e = hipMalloc(&p.d_in_row, rows.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(p.d_tab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(p.d_in_row, rows.data(), rows.size() * 4, hipMemcpyHostToDevice);
+        p.dev_err = e;
+    });
+    if (p.dev_err != hipSuccess) return p.dev_err;
+    GenericArgs a;
+    a.obj_stride = L.obj_stride;
+    a.nvec = (uint32_t)((L.shard_len + 15) / 16);
+    a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
+    a.nw = (uint32_t)s.nw;
+    a.K = (uint32_t)K;
+    a.rstride = (uint32_t)p.R;
+    a.tab = p.d_tab + (size_t)s.r0 * 4;
+    a.in_row = p.d_in_row;
+    a.pitch = (uint32_t)L.pitch;
+    int maxrow = 0;
+    for (int c = 0; c < K; ++c) maxrow = std::max(maxrow, p.in_rows[c]);
+    for (int r = 0; r < R; ++r) {
+        const int row = p.out_rows[s.r0 + r];
+        a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * L.pitch);
+        maxrow = std::max(maxrow, row);
+    }
+    a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * 16);
+    const unsigned gx = (a.nvec + kBlock - 1) / kBlock;
+    for (int o0 = 0; o0 < L.nobj; o0 += kMaxGridY) {
+        const int no = std::min(kMaxGridY, L.nobj - o0);
+        a.base = L.base + (size_t)o0 * L.obj_stride;
+        a.bad = d_bad ? d_bad + o0 : nullptr;
+        hipLaunchKernelGGL((gf_apply_generic<R>), dim3(gx, no), dim3(kBlock), 0, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+typedef hipError_t (*fixed_fn)(const Plan &, const Sub &, const Layout &, uint32_t *, hipStream_t);
+
+template <int K>
+constexpr fixed_fn pick_r(int R) {
+    return R == 1 ? &launch_fixed<K, 1>
+         : R == 2 ? &launch_fixed<K, 2>
+         : R == 3 ? &launch_fixed<K, 3>
+                  : &launch_fixed<K, 4>;
+}
+
+fixed_fn pick_fixed(int K, int R) {
+    switch (K) {
+#define RSGPU_K(k) case k: return pick_r<k>(R);
+        RSGPU_K(1) RSGPU_K(2) RSGPU_K(3) RSGPU_K(4) RSGPU_K(5) RSGPU_K(6) RSGPU_K(7) RSGPU_K(8)
+        RSGPU_K(9) RSGPU_K(10) RSGPU_K(11) RSGPU_K(12) RSGPU_K(13) RSGPU_K(14) RSGPU_K(15)
+        RSGPU_K(16)
+#undef RSGPU_K
+        default: return nullptr;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
+    if (L.nobj <= 0 || p.R <= 0) return hipSuccess;
+    if (p.K <= kMaxK) {
+        // split R into passes of <= 4 rows; written rows first, then checks
+        for (int r0 = 0; r0 < p.R; r0 += kMaxR) {
+            Sub s{r0, std::min(kMaxR, p.R - r0), 0};
+            s.nw = std::max(0, std::min(s.R, p.nw - r0));
+            hipError_t e = pick_fixed(p.K, s.R)(p, s, L, d_bad, st);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    // K > 16: generic kernel, one pass per <= 4 rows over one table image
+    for (int r0 = 0; r0 < p.R; r0 += kMaxR) {
+        Sub s{r0, std::min(kMaxR, p.R - r0), 0};
+        s.nw = std::max(0, std::min(s.R, p.nw - r0));
+        hipError_t e;
+        switch (s.R) {
+            case 1: e = launch_generic<1>(p, s, L, d_bad, st); break;
+            case 2: e = launch_generic<2>(p, s, L, d_bad, st); break;
+            case 3: e = launch_generic<3>(p, s, L, d_bad, st); break;
+            default: e = launch_generic<4>(p, s, L, d_bad, st); break;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace rsgpu

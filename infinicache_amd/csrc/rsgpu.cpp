@@ -1,0 +1,647 @@
+// rsgpu.cpp — host side of the C ABI in include/rsgpu.h.
+//
+// Mirrors reedsolomon.Encoder v1.9.3 (the interface Client.EC holds,
+// /root/reference/client/client.go:38; factory /root/reference/client/ec.go:14-24):
+//   * rsgpu_create       <- reedsolomon.New (buildMatrix; ErrInvShardNum /
+//                           ErrMaxShardNum checks)
+//   * rsgpu_encode       <- Encode           (ecRedis.go:390)
+//   * rsgpu_verify       <- Verify           (ecRedis.go:395,406,420)
+//   * rsgpu_reconstruct  <- Reconstruct / ReconstructData (ecRedis.go:415)
+//   * rsgpu_decode       <- Client.decode's Verify->Reconstruct->Verify
+//                           (ecRedis.go:404-427), fused into one pass
+//   * rsgpu_update       <- Update
+// Argument checks follow upstream precedence (length check, then
+// checkShards).  All GF arithmetic runs in gf_kernels.hip; this file only
+// derives per-operation coefficient matrices (including upstream's
+// per-erasure-pattern inverse cache, inversionTree) and moves bytes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+#include "gf256.h"
+#include "gf_apply.h"
+
+namespace rsgpu {
+
+const GF &gf() {
+    static const GF g;
+    return g;
+}
+
+bool gf_invert(const uint8_t *in, int n, uint8_t *out) {
+    const GF &g = gf();
+    const int cols = 2 * n;
+    std::vector<uint8_t> w((size_t)n * cols, 0);
+    for (int r = 0; r < n; ++r) {
+        std::memcpy(&w[(size_t)r * cols], in + (size_t)r * n, n);
+        w[(size_t)r * cols + n + r] = 1;
+    }
+    for (int r = 0; r < n; ++r) {
+        uint8_t *row = &w[(size_t)r * cols];
+        if (row[r] == 0) {
+            for (int rb = r + 1; rb < n; ++rb)
+                if (w[(size_t)rb * cols + r]) {
+                    std::swap_ranges(row, row + cols, &w[(size_t)rb * cols]);
+                    break;
+                }
+        }
+        if (row[r] == 0) return false;
+        const uint8_t s = g.div(1, row[r]);
+        for (int c = 0; c < cols; ++c) row[c] = g.mul(row[c], s);
+        for (int rb = 0; rb < n; ++rb) {
+            if (rb == r) continue;
+            uint8_t *o = &w[(size_t)rb * cols];
+            const uint8_t f = o[r];
+            if (f)
+                for (int c = 0; c < cols; ++c) o[c] ^= g.mul(f, row[c]);
+        }
+    }
+    for (int r = 0; r < n; ++r) std::memcpy(out + (size_t)r * n, &w[(size_t)r * cols + n], n);
+    return true;
+}
+
+bool gf_build_matrix(int k, int p, unsigned kind, std::vector<uint8_t> &out) {
+    const GF &g = gf();
+    const int n = k + p;
+    out.assign((size_t)n * k, 0);
+    if (kind == RSGPU_MATRIX_CAUCHY || kind == RSGPU_MATRIX_PAR1) {
+        for (int r = 0; r < n; ++r)
+            for (int c = 0; c < k; ++c)
+                out[(size_t)r * k + c] = r < k ? (uint8_t)(r == c)
+                                       : kind == RSGPU_MATRIX_CAUCHY ? g.div(1, (uint8_t)(r ^ c))
+                                                                     : g.pow((uint8_t)(c + 1), r - k);
+        return true;
+    }
+    std::vector<uint8_t> vm((size_t)n * k), inv((size_t)k * k);
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < k; ++c) vm[(size_t)r * k + c] = g.pow((uint8_t)r, c);
+    if (!gf_invert(vm.data(), k, inv.data())) return false;
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < k; ++c) {
+            uint8_t a = 0;
+            for (int i = 0; i < k; ++i) a ^= g.mul(vm[(size_t)r * k + i], inv[(size_t)i * k + c]);
+            out[(size_t)r * k + c] = a;
+        }
+    return true;
+}
+
+}  // namespace rsgpu
+
+using namespace rsgpu;
+
+namespace {
+
+// One staging slot for the host-memory API: pinned host image + device image
+// of an object laid out [row][pitch], a stream and a mismatch flag.
+struct Slot {
+    uint8_t *h = nullptr, *d = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+    uint32_t *d_bad = nullptr, *h_bad = nullptr;
+    ~Slot() {
+        if (stream) (void)hipStreamDestroy(stream);
+        if (h) (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        if (d_bad) (void)hipFree(d_bad);
+        if (h_bad) (void)hipHostFree(h_bad);
+    }
+};
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+bool debug_on() {
+    static const bool on = std::getenv("RSGPU_DEBUG") != nullptr;
+    return on;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    if (debug_on()) std::fprintf(stderr, "rsgpu: %s failed: %s\n", what, hipGetErrorString(e));
+    return RSGPU_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+}  // namespace
+
+struct rsgpu_ctx {
+    int k = 0, p = 0, n = 0;
+    unsigned kind = 0;
+    int device = 0;
+    std::vector<uint8_t> m;  // n x k coding matrix
+
+    std::mutex mu;  // guards everything below
+    std::map<std::string, std::vector<uint8_t>> inverses;  // survivors -> k x k inverse
+    std::map<std::string, std::shared_ptr<Plan>> plans;
+    std::vector<std::unique_ptr<Slot>> free_slots;
+    int dev_state = 0;  // 0 unknown, 1 ok, <0 error code
+
+    const uint8_t *row(int r) const { return &m[(size_t)r * k]; }
+
+    // ---- device bring-up (lazy; per call hipSetDevice for thread safety)
+    int use_device() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (dev_state == 0) dev_state = rsgpu_device_ok(device) ? 1 : RSGPU_ERR_NO_DEVICE;
+            if (dev_state < 0) return dev_state;
+        }
+        HIP_TRY(hipSetDevice(device));
+        return RSGPU_OK;
+    }
+
+    // ---- survivors' inverse (upstream inversionTree.GetInvertedMatrix /
+    // InsertInvertedMatrix, keyed here by the survivor list, which is a
+    // function of upstream's invalidIndices key)
+    int inverse(const std::vector<int> &surv, std::vector<uint8_t> &inv) {
+        std::string key(surv.begin(), surv.end());
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = inverses.find(key);
+            if (it != inverses.end()) { inv = it->second; return RSGPU_OK; }
+        }
+        std::vector<uint8_t> sub((size_t)k * k);
+        for (int i = 0; i < k; ++i) std::memcpy(&sub[(size_t)i * k], row(surv[i]), k);
+        inv.assign((size_t)k * k, 0);
+        if (!gf_invert(sub.data(), k, inv.data())) return RSGPU_ERR_SINGULAR;
+        std::lock_guard<std::mutex> g(mu);
+        inverses.emplace(key, inv);
+        return RSGPU_OK;
+    }
+
+    std::shared_ptr<Plan> cached(const std::string &key) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = plans.find(key);
+        return it == plans.end() ? nullptr : it->second;
+    }
+    std::shared_ptr<Plan> remember(const std::string &key, std::shared_ptr<Plan> p) {
+        p->build_tables();
+        std::lock_guard<std::mutex> g(mu);
+        return plans.emplace(key, std::move(p)).first->second;
+    }
+
+    // Encode: rows [k, n) <- M[k:] x rows [0, k)
+    std::shared_ptr<Plan> plan_encode() {
+        if (auto p = cached("E")) return p;
+        auto p = std::make_shared<Plan>();
+        p->K = k; p->R = this->p; p->nw = this->p;
+        for (int c = 0; c < k; ++c) p->in_rows.push_back(c);
+        for (int r = k; r < n; ++r) {
+            p->out_rows.push_back(r);
+            p->coef.insert(p->coef.end(), row(r), row(r) + k);
+        }
+        return remember("E", p);
+    }
+
+    // Verify: check rows M[j] x data XOR parity_j == 0 for j in [k, n)
+    std::shared_ptr<Plan> plan_verify() {
+        if (auto p = cached("V")) return p;
+        auto p = std::make_shared<Plan>();
+        p->K = n; p->R = this->p; p->nw = 0;
+        for (int c = 0; c < n; ++c) p->in_rows.push_back(c);
+        for (int j = k; j < n; ++j) {
+            p->out_rows.push_back(-1);
+            for (int c = 0; c < n; ++c) p->coef.push_back(c < k ? row(j)[c] : (uint8_t)(c == j));
+        }
+        return remember("V", p);
+    }
+
+    // Reconstruct (upstream reconstruct()): survivors = first k present rows.
+    // Missing data row i = inv[i] x survivors; missing parity row j =
+    // (M[j] x inv) x survivors — the same bytes as upstream's second
+    // codeSomeShards over the (reconstructed) data rows, in one pass.
+    // With check = true (fused Client.decode), every present row beyond
+    // the survivors becomes a check row (M[j] x inv) x survivors XOR row_j:
+    // exactly the comparisons upstream's Verify-after-Reconstruct can fail;
+    // the survivors' own comparisons are identities (M[V] x inv = I).
+    int plan_reconstruct(const uint8_t *present, bool data_only, bool check,
+                         std::shared_ptr<Plan> &out) {
+        std::string key = check ? "D" : (data_only ? "d" : "R");
+        for (int i = 0; i < n; ++i) key.push_back(present[i] ? '1' : '0');
+        if ((out = cached(key))) return RSGPU_OK;
+        std::vector<int> surv, extra, miss;
+        for (int i = 0; i < n; ++i) {
+            if (present[i]) (surv.size() < (size_t)k ? surv : extra).push_back(i);
+            else miss.push_back(i);
+        }
+        std::vector<uint8_t> inv;
+        int e = inverse(surv, inv);
+        if (e) return e;
+        const GF &g = gf();
+        auto p = std::make_shared<Plan>();
+        p->in_rows = surv;
+        if (check) p->in_rows.insert(p->in_rows.end(), extra.begin(), extra.end());
+        p->K = (int)p->in_rows.size();
+        // coefficient row over survivors for an arbitrary matrix row j
+        auto over_surv = [&](int j, std::vector<uint8_t> &cr) {
+            cr.assign(p->K, 0);
+            if (j < k) {
+                std::memcpy(cr.data(), &inv[(size_t)j * k], k);
+                return;
+            }
+            for (int c = 0; c < k; ++c) {
+                const uint8_t mj = row(j)[c];
+                if (!mj) continue;
+                for (int s = 0; s < k; ++s) cr[s] ^= g.mul(mj, inv[(size_t)c * k + s]);
+            }
+        };
+        std::vector<uint8_t> cr;
+        for (int i : miss) {
+            if (data_only && i >= k) continue;
+            over_surv(i, cr);
+            p->out_rows.push_back(i);
+            p->coef.insert(p->coef.end(), cr.begin(), cr.end());
+        }
+        p->nw = (int)p->out_rows.size();
+        if (check) {
+            for (size_t x = 0; x < extra.size(); ++x) {
+                const int j = extra[x];
+                if (j < k) continue;  // upstream Verify compares parity rows only
+                over_surv(j, cr);
+                cr[k + x] ^= 1;
+                p->out_rows.push_back(-1);
+                p->coef.insert(p->coef.end(), cr.begin(), cr.end());
+            }
+        }
+        p->R = (int)p->out_rows.size();
+        out = remember(key, p);
+        return RSGPU_OK;
+    }
+
+    // ---- staging slots
+    int get_slot(size_t bytes, std::unique_ptr<Slot> &s) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_slots.empty()) { s = std::move(free_slots.back()); free_slots.pop_back(); }
+        }
+        if (!s) {
+            s.reset(new Slot());
+            HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+            HIP_TRY(hipMalloc(&s->d_bad, 4));
+            HIP_TRY(hipHostMalloc(&s->h_bad, 4, hipHostMallocDefault));
+        }
+        if (s->cap < bytes) {
+            if (s->h) (void)hipHostFree(s->h);
+            if (s->d) (void)hipFree(s->d);
+            s->h = nullptr; s->d = nullptr; s->cap = 0;
+            const size_t cap = round_up(bytes, (size_t)1 << 20);
+            HIP_TRY(hipHostMalloc(&s->h, cap, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&s->d, cap));
+            s->cap = cap;
+        }
+        return RSGPU_OK;
+    }
+    void put_slot(std::unique_ptr<Slot> s) {
+        std::lock_guard<std::mutex> g(mu);
+        free_slots.push_back(std::move(s));
+    }
+};
+
+namespace {
+
+// upstream checkShards(shards, nilok): size = first non-empty length
+int check_shards(const size_t *lens, int n, bool nilok, size_t *size) {
+    size_t s = 0;
+    for (int i = 0; i < n; ++i)
+        if (lens[i]) { s = lens[i]; break; }
+    if (s == 0) return RSGPU_ERR_SHARD_NO_DATA;
+    for (int i = 0; i < n; ++i)
+        if (lens[i] != s && (lens[i] != 0 || !nilok)) return RSGPU_ERR_SHARD_SIZE;
+    *size = s;
+    return RSGPU_OK;
+}
+
+// Runs `plan` over one object staged from host buffers.  in_src[c] is the
+// host source of staging row plan.in_rows[c]; out_dst[r] receives written
+// row r.  Returns the mismatch flag in *bad when the plan has check rows.
+int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
+             const std::vector<const uint8_t *> &in_src, const std::vector<uint8_t *> &out_dst,
+             uint32_t *bad) {
+    const size_t pitch = round_up(size, 256);
+    std::unique_ptr<Slot> s;
+    int e = ctx->get_slot((size_t)nrows_staged * pitch, s);
+    if (e) return e;
+    const size_t vec_bytes = round_up(size, 16);
+    // stage inputs (zero the vector tail so check rows see clean pads)
+    for (int c = 0; c < plan.K; ++c) {
+        uint8_t *dst = s->h + (size_t)plan.in_rows[c] * pitch;
+        std::memcpy(dst, in_src[c], size);
+        if (vec_bytes > size) std::memset(dst + size, 0, vec_bytes - size);
+    }
+    // H2D the staged input rows, merging contiguous runs
+    std::vector<int> rows(plan.in_rows);
+    std::sort(rows.begin(), rows.end());
+    for (size_t i = 0; i < rows.size();) {
+        size_t j = i + 1;
+        while (j < rows.size() && rows[j] == rows[j - 1] + 1) ++j;
+        const size_t off = (size_t)rows[i] * pitch, len = (size_t)(rows[j - 1] - rows[i]) * pitch + vec_bytes;
+        if (hipMemcpyAsync(s->d + off, s->h + off, len, hipMemcpyHostToDevice, s->stream) != hipSuccess) {
+            ctx->put_slot(std::move(s));
+            return RSGPU_ERR_HIP;
+        }
+        i = j;
+    }
+    hipError_t he = hipSuccess;
+    if (plan.nw < plan.R) he = hipMemsetAsync(s->d_bad, 0, 4, s->stream);
+    Layout L{s->d, 0, pitch, size, 1};
+    if (he == hipSuccess) he = launch_plan(plan, L, s->d_bad, s->stream);
+    for (int r = 0; r < plan.nw && he == hipSuccess; ++r) {
+        const size_t off = (size_t)plan.out_rows[r] * pitch;
+        he = hipMemcpyAsync(s->h + off, s->d + off, size, hipMemcpyDeviceToHost, s->stream);
+    }
+    if (he == hipSuccess && plan.nw < plan.R)
+        he = hipMemcpyAsync(s->h_bad, s->d_bad, 4, hipMemcpyDeviceToHost, s->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
+    if (he != hipSuccess) {
+        ctx->put_slot(std::move(s));
+        return hip_fail(he, "run_host");
+    }
+    for (int r = 0; r < plan.nw; ++r) std::memcpy(out_dst[r], s->h + (size_t)plan.out_rows[r] * pitch, size);
+    if (bad) *bad = plan.nw < plan.R ? *s->h_bad : 0;
+    ctx->put_slot(std::move(s));
+    return RSGPU_OK;
+}
+
+int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_t pitch,
+                 size_t obj_stride, int nobj) {
+    if (!base || nobj < 0) return RSGPU_ERR_INVALID_ARG;
+    if (shard_len == 0) return RSGPU_ERR_SHARD_NO_DATA;
+    if (((uintptr_t)base & 15) || (pitch & 15) || (obj_stride & 15)) return RSGPU_ERR_INVALID_ARG;
+    if (pitch < round_up(shard_len, 16)) return RSGPU_ERR_INVALID_ARG;
+    if ((size_t)ctx->n * pitch >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
+    if (nobj > 1 && obj_stride < (size_t)ctx->n * pitch) return RSGPU_ERR_INVALID_ARG;
+    return RSGPU_OK;
+}
+
+}  // namespace
+
+// ============================================================== C ABI
+
+extern "C" {
+
+int rsgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rsgpu_device_ok(int device) {
+    const int n = rsgpu_device_count();
+    if (device < 0 || device >= n) return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+const char *rsgpu_strerror(int code) {
+    switch (code) {
+        case RSGPU_OK: return "ok";
+        case RSGPU_ERR_INV_SHARD_NUM: return "cannot create Encoder with zero or less data/parity shards";
+        case RSGPU_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+        case RSGPU_ERR_TOO_FEW_SHARDS: return "too few shards given";
+        case RSGPU_ERR_SHARD_NO_DATA: return "no shard data";
+        case RSGPU_ERR_SHARD_SIZE: return "shard sizes do not match";
+        case RSGPU_ERR_SINGULAR: return "matrix is singular";
+        case RSGPU_ERR_SHORT_DATA: return "not enough data to fill the number of requested shards";
+        case RSGPU_ERR_RECONSTRUCT_REQUIRED: return "reconstruction required as one or more required data shards are nil";
+        case RSGPU_ERR_INVALID_INPUT: return "invalid input";
+        case RSGPU_ERR_NOT_IMPLEMENTED: return "Not implemented";
+        case RSGPU_ERR_INVALID_ARG: return "rsgpu: invalid argument";
+        case RSGPU_ERR_NO_DEVICE: return "rsgpu: no usable gfx950 device";
+        case RSGPU_ERR_HIP: return "rsgpu: HIP runtime error";
+        case RSGPU_ERR_NOMEM: return "rsgpu: out of memory";
+        default: return "rsgpu: unknown error";
+    }
+}
+
+int rsgpu_create(int data_shards, int parity_shards, int device, unsigned flags, rsgpu_ctx **out) {
+    if (!out) return RSGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (data_shards <= 0 || parity_shards <= 0) return RSGPU_ERR_INV_SHARD_NUM;
+    if (data_shards + parity_shards > 256) return RSGPU_ERR_MAX_SHARD_NUM;
+    const unsigned kind = flags & RSGPU_MATRIX_MASK;
+    if (kind > RSGPU_MATRIX_PAR1 || (flags & ~RSGPU_MATRIX_MASK)) return RSGPU_ERR_INVALID_ARG;
+    if (device < 0) return RSGPU_ERR_INVALID_ARG;
+    std::unique_ptr<rsgpu_ctx> c(new (std::nothrow) rsgpu_ctx());
+    if (!c) return RSGPU_ERR_NOMEM;
+    c->k = data_shards;
+    c->p = parity_shards;
+    c->n = data_shards + parity_shards;
+    c->kind = kind;
+    c->device = device;
+    if (!gf_build_matrix(c->k, c->p, kind, c->m)) return RSGPU_ERR_SINGULAR;
+    *out = c.release();
+    return RSGPU_OK;
+}
+
+void rsgpu_destroy(rsgpu_ctx *ctx) {
+    if (!ctx) return;
+    if (ctx->dev_state == 1) (void)hipSetDevice(ctx->device);
+    delete ctx;
+}
+
+int rsgpu_data_shards(const rsgpu_ctx *ctx) { return ctx ? ctx->k : RSGPU_ERR_INVALID_ARG; }
+int rsgpu_parity_shards(const rsgpu_ctx *ctx) { return ctx ? ctx->p : RSGPU_ERR_INVALID_ARG; }
+
+int rsgpu_matrix(const rsgpu_ctx *ctx, uint8_t *out) {
+    if (!ctx || !out) return RSGPU_ERR_INVALID_ARG;
+    std::memcpy(out, ctx->m.data(), ctx->m.size());
+    return RSGPU_OK;
+}
+
+int rsgpu_encode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards) {
+    if (!ctx || !shards || !lens) return RSGPU_ERR_INVALID_ARG;
+    if (nshards != ctx->n) return RSGPU_ERR_TOO_FEW_SHARDS;
+    size_t size;
+    int e = check_shards(lens, nshards, false, &size);
+    if (e) return e;
+    if ((e = ctx->use_device())) return e;
+    auto plan = ctx->plan_encode();
+    std::vector<const uint8_t *> in(shards, shards + ctx->k);
+    std::vector<uint8_t *> out(shards + ctx->k, shards + ctx->n);
+    return run_host(ctx, *plan, ctx->n, size, in, out, nullptr);
+}
+
+int rsgpu_verify(rsgpu_ctx *ctx, const uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
+    if (!ctx || !shards || !lens || !ok) return RSGPU_ERR_INVALID_ARG;
+    *ok = 0;
+    if (nshards != ctx->n) return RSGPU_ERR_TOO_FEW_SHARDS;
+    size_t size;
+    int e = check_shards(lens, nshards, false, &size);
+    if (e) return e;
+    if ((e = ctx->use_device())) return e;
+    auto plan = ctx->plan_verify();
+    std::vector<const uint8_t *> in(shards, shards + ctx->n);
+    uint32_t bad = 1;
+    e = run_host(ctx, *plan, ctx->n, size, in, {}, &bad);
+    if (e) return e;
+    *ok = bad == 0;
+    return RSGPU_OK;
+}
+
+static int reconstruct_common(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens,
+                              int nshards, bool data_only, bool check, int *ok) {
+    if (!ctx || !shards || !lens) return RSGPU_ERR_INVALID_ARG;
+    if (nshards != ctx->n) return RSGPU_ERR_TOO_FEW_SHARDS;
+    size_t size;
+    int e = check_shards(lens, nshards, true, &size);
+    if (e) return e;
+    std::vector<uint8_t> present(ctx->n);
+    int np = 0;
+    for (int i = 0; i < ctx->n; ++i) np += (present[i] = lens[i] != 0);
+    if (np == ctx->n) {
+        if (!check) return RSGPU_OK;
+        return rsgpu_verify(ctx, shards, lens, nshards, ok);
+    }
+    if (np < ctx->k) return RSGPU_ERR_TOO_FEW_SHARDS;
+    std::shared_ptr<Plan> plan;
+    if ((e = ctx->plan_reconstruct(present.data(), data_only, check, plan))) return e;
+    for (int r = 0; r < plan->nw; ++r)
+        if (!shards[plan->out_rows[r]]) return RSGPU_ERR_INVALID_ARG;
+    if ((e = ctx->use_device())) return e;
+    std::vector<const uint8_t *> in;
+    for (int row : plan->in_rows) in.push_back(shards[row]);
+    std::vector<uint8_t *> out;
+    for (int r = 0; r < plan->nw; ++r) out.push_back(shards[plan->out_rows[r]]);
+    uint32_t bad = 0;
+    e = run_host(ctx, *plan, ctx->n, size, in, out, &bad);
+    if (e) return e;
+    if (ok) *ok = bad == 0;
+    return RSGPU_OK;
+}
+
+int rsgpu_reconstruct(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
+                      int data_only) {
+    return reconstruct_common(ctx, shards, lens, nshards, data_only != 0, false, nullptr);
+}
+
+int rsgpu_decode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
+    if (!ok) return RSGPU_ERR_INVALID_ARG;
+    *ok = 0;
+    return reconstruct_common(ctx, shards, lens, nshards, false, true, ok);
+}
+
+int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
+                 const uint8_t *const *newdata, const size_t *new_lens, int nnew) {
+    if (!ctx || !shards || !lens || !newdata || !new_lens) return RSGPU_ERR_INVALID_ARG;
+    const int k = ctx->k, n = ctx->n;
+    if (nshards != n) return RSGPU_ERR_TOO_FEW_SHARDS;
+    if (nnew != k) return RSGPU_ERR_TOO_FEW_SHARDS;
+    size_t size, size2;
+    int e = check_shards(lens, nshards, true, &size);
+    if (e) return e;
+    if ((e = check_shards(new_lens, nnew, true, &size2))) return e;
+    for (int i = 0; i < k; ++i)
+        if (new_lens[i] != 0 && lens[i] == 0) return RSGPU_ERR_INVALID_INPUT;
+    for (int i = k; i < n; ++i)
+        if (lens[i] == 0) return RSGPU_ERR_INVALID_INPUT;
+    if (size2 != size) return RSGPU_ERR_SHARD_SIZE;
+    std::vector<int> changed;
+    for (int c = 0; c < k; ++c)
+        if (new_lens[c]) changed.push_back(c);
+    if (changed.empty()) return RSGPU_OK;
+    if ((e = ctx->use_device())) return e;
+    // staging rows: [0,n) shards, [n, n+k) new data, [n+k, n+k+|C|+p) outputs
+    const int nc = (int)changed.size();
+    Plan plan;
+    for (int c : changed) plan.in_rows.push_back(c);
+    for (int c : changed) plan.in_rows.push_back(n + c);
+    for (int r = k; r < n; ++r) plan.in_rows.push_back(r);
+    plan.K = (int)plan.in_rows.size();
+    for (int i = 0; i < nc; ++i) {  // delta_c = old_c ^ new_c
+        plan.out_rows.push_back(n + k + i);
+        for (int c = 0; c < plan.K; ++c) plan.coef.push_back(c == i || c == nc + i);
+    }
+    for (int r = 0; r < ctx->p; ++r) {  // parity_r ^= M[k+r][c] (old_c ^ new_c)
+        plan.out_rows.push_back(n + k + nc + r);
+        for (int i = 0; i < nc; ++i) plan.coef.push_back(ctx->row(k + r)[changed[i]]);
+        for (int i = 0; i < nc; ++i) plan.coef.push_back(ctx->row(k + r)[changed[i]]);
+        for (int j = 0; j < ctx->p; ++j) plan.coef.push_back(j == r);
+    }
+    plan.R = plan.nw = nc + ctx->p;
+    plan.build_tables();
+    std::vector<const uint8_t *> in;
+    for (int c : changed) in.push_back(shards[c]);
+    for (int c : changed) in.push_back(newdata[c]);
+    for (int r = k; r < n; ++r) in.push_back(shards[r]);
+    std::vector<uint8_t *> out;
+    for (int c : changed) out.push_back(shards[c]);
+    for (int r = k; r < n; ++r) out.push_back(shards[r]);
+    return run_host(ctx, plan, n + k + nc + ctx->p, size, in, out, nullptr);
+}
+
+// ---------------------------------------------------- device-resident API
+
+int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitch,
+                     size_t obj_stride, int nobj, void *stream) {
+    if (!ctx) return RSGPU_ERR_INVALID_ARG;
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    if (e) return e;
+    if ((e = ctx->use_device())) return e;
+    auto plan = ctx->plan_encode();
+    Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
+    HIP_TRY(launch_plan(*plan, L, nullptr, (hipStream_t)stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_verify_dev(rsgpu_ctx *ctx, const void *d_base, size_t shard_len, size_t pitch,
+                     size_t obj_stride, int nobj, uint32_t *d_bad, void *stream) {
+    if (!ctx || !d_bad) return RSGPU_ERR_INVALID_ARG;
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    if (e) return e;
+    if ((e = ctx->use_device())) return e;
+    auto plan = ctx->plan_verify();
+    Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
+    HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
+    HIP_TRY(launch_plan(*plan, L, d_bad, (hipStream_t)stream));
+    return RSGPU_OK;
+}
+
+static int recon_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                     size_t pitch, size_t obj_stride, int nobj, bool data_only, bool check,
+                     uint32_t *d_bad, void *stream) {
+    if (!ctx || !present) return RSGPU_ERR_INVALID_ARG;
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    if (e) return e;
+    int np = 0;
+    for (int i = 0; i < ctx->n; ++i) np += present[i] != 0;
+    if (np < ctx->k) return RSGPU_ERR_TOO_FEW_SHARDS;
+    if ((e = ctx->use_device())) return e;
+    if (np == ctx->n) {
+        if (!check) return RSGPU_OK;
+        return rsgpu_verify_dev(ctx, d_base, shard_len, pitch, obj_stride, nobj, d_bad, stream);
+    }
+    std::shared_ptr<Plan> plan;
+    if ((e = ctx->plan_reconstruct(present, data_only, check, plan))) return e;
+    Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
+    if (check) HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
+    HIP_TRY(launch_plan(*plan, L, d_bad, (hipStream_t)stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                          size_t pitch, size_t obj_stride, int nobj, int data_only, void *stream) {
+    return recon_dev(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, data_only != 0, false,
+                     nullptr, stream);
+}
+
+int rsgpu_decode_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                     size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream) {
+    if (!d_bad) return RSGPU_ERR_INVALID_ARG;
+    return recon_dev(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, false, true, d_bad,
+                     stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,406 @@
+"""Host-side mirror of the InfiniCache client's erasure-coding interface.
+
+Mirrors, name for name:
+  * reedsolomon.Encoder (klauspost/reedsolomon v1.9.3, the interface held in
+    Client.EC, /root/reference/client/client.go:38): Encode, Verify,
+    Reconstruct, ReconstructData, Update, Split, Join;
+  * reedsolomon.New(dataShards, parityShards, opts...) -> ``New``;
+  * client.NewEncoder (/root/reference/client/ec.go:14-24) -> ``NewEncoder``;
+  * client.DummyEncoder (/root/reference/client/ec.go:26-121) -> ``DummyEncoder``.
+
+Encode/Verify/Reconstruct/ReconstructData/Update run on the MI355X through the
+C ABI in include/rsgpu.h (librsgpu.so); Split/Join are host slicing, exactly
+as in the Go shim design.  Go errors become exceptions of the
+same names; Verify returns a bool and raises where Go returns (false, err).
+There is no CPU fallback: on a machine without a gfx950 device the compute
+methods raise NoDevice.
+
+Batched device-resident entry points (``encode_dev`` & co.) take a device
+pointer (int) or any object with ``data_ptr()`` (a torch tensor) laid out
+[object][shard][pitch] in HBM.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+# ------------------------------------------------------------------ errors
+
+
+class RSError(Exception):
+    """Base of the codec errors; ``code`` is the RSGPU_ERR_* value."""
+    code = 0
+
+    def __init__(self, msg: Optional[str] = None):
+        super().__init__(msg or self.__class__.__doc__)
+
+
+class ErrInvShardNum(RSError):
+    """cannot create Encoder with zero or less data/parity shards"""
+    code = -1
+
+
+class ErrMaxShardNum(RSError):
+    """cannot create Encoder with more than 256 data+parity shards"""
+    code = -2
+
+
+class ErrTooFewShards(RSError):
+    """too few shards given"""
+    code = -3
+
+
+class ErrShardNoData(RSError):
+    """no shard data"""
+    code = -4
+
+
+class ErrShardSize(RSError):
+    """shard sizes do not match"""
+    code = -5
+
+
+class ErrSingular(RSError):
+    """matrix is singular"""
+    code = -6
+
+
+class ErrShortData(RSError):
+    """not enough data to fill the number of requested shards"""
+    code = -7
+
+
+class ErrReconstructRequired(RSError):
+    """reconstruction required as one or more required data shards are nil"""
+    code = -8
+
+
+class ErrInvalidInput(RSError):
+    """invalid input"""
+    code = -9
+
+
+class ErrNotImplemented(RSError):
+    """Not implemented"""
+    code = -10
+
+
+class InvalidArgument(RSError):
+    """rsgpu: invalid argument"""
+    code = -20
+
+
+class NoDevice(RSError):
+    """rsgpu: no usable gfx950 device"""
+    code = -21
+
+
+class HipError(RSError):
+    """rsgpu: HIP runtime error"""
+    code = -22
+
+
+class OutOfMemory(RSError):
+    """rsgpu: out of memory"""
+    code = -23
+
+
+_ERRORS = {c.code: c for c in (ErrInvShardNum, ErrMaxShardNum, ErrTooFewShards, ErrShardNoData,
+                               ErrShardSize, ErrSingular, ErrShortData, ErrReconstructRequired,
+                               ErrInvalidInput, ErrNotImplemented, InvalidArgument, NoDevice,
+                               HipError, OutOfMemory)}
+
+
+def _check(code: int):
+    if code != 0:
+        cls = _ERRORS.get(code, RSError)
+        raise cls()
+
+
+MATRIX_KINDS = {"vandermonde": 0, "cauchy": 1, "par1": 2}
+
+# ---------------------------------------------------------------- helpers
+
+
+def _as_u8(buf, writable: bool) -> Optional[np.ndarray]:
+    """View a shard buffer as a 1-D uint8 numpy array (no copy)."""
+    if buf is None:
+        return None
+    if isinstance(buf, np.ndarray):
+        a = buf
+        if a.dtype != np.uint8 or a.ndim != 1 or not a.flags.c_contiguous:
+            a = a.reshape(-1).view(np.uint8)
+    else:
+        a = np.frombuffer(buf, dtype=np.uint8)
+    if writable and not a.flags.writeable and len(a):
+        raise InvalidArgument("output shard buffer is read-only")
+    return a
+
+
+class _ShardTable:
+    """Pointer + length arrays for a list of shards (None/empty => len 0)."""
+
+    def __init__(self, shards, writable_idx=()):
+        self.arrs: List[Optional[np.ndarray]] = []
+        n = len(shards)
+        self.ptrs = (_lib.u8p * n)()
+        self.lens = (ctypes.c_size_t * n)()
+        for i, s in enumerate(shards):
+            a = _as_u8(s, i in writable_idx)
+            self.arrs.append(a)
+            if a is not None and len(a):
+                self.ptrs[i] = a.ctypes.data_as(_lib.u8p)
+                self.lens[i] = len(a)
+            else:
+                self.lens[i] = 0
+
+
+def _dptr(x) -> int:
+    if x is None:
+        return 0
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    return int(x)
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        return 0
+    if hasattr(stream, "cuda_stream"):
+        return int(stream.cuda_stream)
+    return int(stream)
+
+
+def device_count() -> int:
+    return _lib.load().rsgpu_device_count()
+
+
+def device_ok(device: int = 0) -> bool:
+    return bool(_lib.load().rsgpu_device_ok(device))
+
+# ---------------------------------------------------------------- encoder
+
+
+class RSEncoder:
+    """reedsolomon.Encoder backed by the gfx950 kernels (reedsolomon.New)."""
+
+    def __init__(self, data_shards: int, parity_shards: int, *, device: int = 0,
+                 matrix: str = "vandermonde", max_goroutines: int = 0):
+        L = _lib.load()
+        self._L = L
+        ctx = ctypes.c_void_p()
+        _check(L.rsgpu_create(data_shards, parity_shards, device, MATRIX_KINDS[matrix],
+                              ctypes.byref(ctx)))
+        self._ctx = ctx
+        self.DataShards = data_shards
+        self.ParityShards = parity_shards
+        self.Shards = data_shards + parity_shards
+        self.device = device
+        # upstream WithMaxGoroutines has no GPU meaning; kept for API parity
+        self.max_goroutines = max_goroutines
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx:
+            self._L.rsgpu_destroy(ctx)
+            self._ctx = None
+
+    def matrix(self) -> np.ndarray:
+        out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
+        _check(self._L.rsgpu_matrix(self._ctx, out.ctypes.data_as(_lib.u8p)))
+        return out
+
+    # -- the 7 reedsolomon.Encoder methods -------------------------------
+    def Encode(self, shards: Sequence) -> None:
+        t = _ShardTable(shards, writable_idx=range(self.DataShards, len(shards)))
+        _check(self._L.rsgpu_encode(self._ctx, t.ptrs, t.lens, len(shards)))
+
+    def Verify(self, shards: Sequence) -> bool:
+        t = _ShardTable(shards)
+        ok = ctypes.c_int(0)
+        _check(self._L.rsgpu_verify(self._ctx, t.ptrs, t.lens, len(shards), ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def _prepare_missing(self, shards: list, data_only: bool):
+        """upstream reconstruct(): missing shards get a buffer of the shard
+        size (re-using capacity is a Go notion; Python allocates)."""
+        size = next((len(s) for s in shards if s is not None and len(s)), 0)
+        bufs = list(shards)
+        missing = []
+        if size:
+            for i, s in enumerate(shards):
+                if s is None or len(s) == 0:
+                    if data_only and i >= self.DataShards:
+                        continue
+                    bufs[i] = np.zeros(size, dtype=np.uint8)
+                    missing.append(i)
+        return bufs, missing
+
+    def _reconstruct(self, shards: list, data_only: bool, fused_verify: bool):
+        if not isinstance(shards, list):
+            raise InvalidArgument("shards must be a list (filled in place)")
+        bufs, missing = self._prepare_missing(shards, data_only)
+        n = len(shards)
+        ptrs = (_lib.u8p * n)()
+        lens = (ctypes.c_size_t * n)()
+        arrs = []
+        for i in range(n):
+            a = _as_u8(bufs[i], i in missing)
+            arrs.append(a)
+            if a is not None and len(a):
+                ptrs[i] = a.ctypes.data_as(_lib.u8p)
+                lens[i] = 0 if i in missing else len(a)
+        ok = ctypes.c_int(1)
+        if fused_verify:
+            _check(self._L.rsgpu_decode(self._ctx, ptrs, lens, n, ctypes.byref(ok)))
+        else:
+            _check(self._L.rsgpu_reconstruct(self._ctx, ptrs, lens, n, int(data_only)))
+        for i in missing:
+            shards[i] = bufs[i]
+        return bool(ok.value)
+
+    def Reconstruct(self, shards: list) -> None:
+        self._reconstruct(shards, data_only=False, fused_verify=False)
+
+    def ReconstructData(self, shards: list) -> None:
+        self._reconstruct(shards, data_only=True, fused_verify=False)
+
+    def DecodeVerify(self, shards: list) -> bool:
+        """Client.decode's Reconstruct + Verify (ecRedis.go:415-420) fused in
+        one device pass; returns what the Verify after Reconstruct returns."""
+        return self._reconstruct(shards, data_only=False, fused_verify=True)
+
+    def Update(self, shards: Sequence, newDatashards: Sequence) -> None:
+        t = _ShardTable(shards, writable_idx=range(len(shards)))
+        nt = _ShardTable(newDatashards)
+        _check(self._L.rsgpu_update(self._ctx, t.ptrs, t.lens, len(shards), nt.ptrs, nt.lens,
+                                    len(newDatashards)))
+
+    def Split(self, data) -> List[np.ndarray]:
+        """upstream Split: perShard = ceil(len/k); zero-pad to (k+p)*perShard;
+        k+p consecutive views of ONE backing array.  (Go's cap(data) > len
+        quirk does not arise: Python buffers have no spare capacity.)"""
+        d = _as_u8(data, False)
+        if d is None or len(d) == 0:
+            raise ErrShortData()
+        per = (len(d) + self.DataShards - 1) // self.DataShards
+        buf = np.zeros(self.Shards * per, dtype=np.uint8)
+        buf[:len(d)] = d
+        return [buf[i * per:(i + 1) * per] for i in range(self.Shards)]
+
+    def Join(self, dst, shards: Sequence, outSize: int) -> None:
+        _join(self.DataShards, dst, shards, outSize)
+
+    # -- batched device-resident API (HBM in, HBM out) --------------------
+    def encode_dev(self, base, shard_len, pitch, obj_stride, nobj, stream=None):
+        _check(self._L.rsgpu_encode_dev(self._ctx, _dptr(base), shard_len, pitch, obj_stride, nobj,
+                                        _stream_handle(stream)))
+
+    def verify_dev(self, base, shard_len, pitch, obj_stride, nobj, bad, stream=None):
+        _check(self._L.rsgpu_verify_dev(self._ctx, _dptr(base), shard_len, pitch, obj_stride, nobj,
+                                        _dptr(bad), _stream_handle(stream)))
+
+    def reconstruct_dev(self, base, present, shard_len, pitch, obj_stride, nobj, data_only=False,
+                        stream=None):
+        pr = (ctypes.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
+        _check(self._L.rsgpu_reconstruct_dev(self._ctx, _dptr(base), pr, shard_len, pitch,
+                                             obj_stride, nobj, int(data_only),
+                                             _stream_handle(stream)))
+
+    def decode_dev(self, base, present, shard_len, pitch, obj_stride, nobj, bad, stream=None):
+        pr = (ctypes.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
+        _check(self._L.rsgpu_decode_dev(self._ctx, _dptr(base), pr, shard_len, pitch, obj_stride,
+                                        nobj, _dptr(bad), _stream_handle(stream)))
+
+
+def _join(k: int, dst, shards: Sequence, outSize: int) -> None:
+    """upstream Join (identical logic in /root/reference/client/ec.go:83-121)."""
+    if len(shards) < k:
+        raise ErrTooFewShards()
+    shards = shards[:k]
+    size = 0
+    for s in shards:
+        if s is None:
+            raise ErrReconstructRequired()
+        size += len(s)
+        if size >= outSize:
+            break
+    if size < outSize:
+        raise ErrShortData()
+    write = outSize
+    for s in shards:
+        if write < len(s):
+            dst.write(bytes(memoryview(_as_u8(s, False))[:write]))
+            return
+        dst.write(bytes(_as_u8(s, False)))
+        write -= len(s)
+
+
+def New(dataShards: int, parityShards: int, *, device: int = 0, matrix: str = "vandermonde",
+        max_goroutines: int = 0) -> RSEncoder:
+    """reedsolomon.New: raises ErrInvShardNum / ErrMaxShardNum."""
+    return RSEncoder(dataShards, parityShards, device=device, matrix=matrix,
+                     max_goroutines=max_goroutines)
+
+
+class DummyEncoder:
+    """client.DummyEncoder (/root/reference/client/ec.go:26-121): the p == 0
+    codec — no parity, Verify only checks shard presence."""
+
+    def __init__(self, DataShards: int):
+        self.DataShards = DataShards
+
+    def Encode(self, shards):
+        return None
+
+    def Verify(self, shards) -> bool:
+        if len(shards) != self.DataShards:
+            raise ErrTooFewShards()
+        for s in shards:
+            if s is None or len(s) == 0:
+                raise ErrTooFewShards()
+        return True
+
+    def Reconstruct(self, shards):
+        self.Verify(shards)
+
+    def ReconstructData(self, shards):
+        self.Verify(shards)
+
+    def Update(self, shards, newDatashards):
+        raise ErrNotImplemented()
+
+    def Split(self, data):
+        d = _as_u8(data, False)
+        if d is None or len(d) == 0:
+            raise ErrShortData()
+        per = (len(d) + self.DataShards - 1) // self.DataShards
+        dst: List[Optional[np.ndarray]] = [None] * self.DataShards
+        i = 0
+        while i < len(dst) and len(d) >= per:
+            dst[i] = d[:per]
+            d = d[per:]
+            i += 1
+        if i < len(dst):
+            dst[i] = d
+        return dst
+
+    def Join(self, dst, shards, outSize):
+        _join(self.DataShards, dst, shards, outSize)
+
+
+def NewEncoder(dataShards: int, parityShards: int, ecMaxGoroutine: int, *, device: int = 0):
+    """client.NewEncoder (/root/reference/client/ec.go:14-24): p == 0 ->
+    DummyEncoder; otherwise New(...), printing and swallowing the error (the
+    Go factory then returns a nil Encoder, here None)."""
+    if parityShards == 0:
+        return DummyEncoder(dataShards)
+    try:
+        return New(dataShards, parityShards, device=device, max_goroutines=ecMaxGoroutine)
+    except RSError as err:
+        print("newEncoder err", err)
+        return None

@@ -1,0 +1,123 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+entry point include/rsgpu.h declares, follows upstream error precedence
+before touching a device, and builds the same coding matrices as the
+oracle.  (No compute calls succeed without a device: they must fail loudly
+with RSGPU_ERR_NO_DEVICE — there is no CPU fallback.)"""
+import ctypes
+import re
+
+import numpy as np
+import pytest
+
+import infinicache_amd as ia
+import oracle
+from infinicache_amd import _lib
+
+
+def declared_functions():
+    src = open(_lib.HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rsgpu_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_exports():
+    assert declared_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(L, name), name
+
+
+def test_library_has_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_error_codes_match_oracle_and_header():
+    src = open(_lib.HEADER).read()
+    codes = dict((m[0], int(m[1])) for m in re.findall(r"#define (RSGPU_ERR_\w+) (-?\d+)", src))
+    assert codes["RSGPU_ERR_TOO_FEW_SHARDS"] == oracle.ERR_TOO_FEW_SHARDS == ia.ErrTooFewShards.code
+    assert codes["RSGPU_ERR_SHARD_SIZE"] == oracle.ERR_SHARD_SIZE == ia.ErrShardSize.code
+    assert codes["RSGPU_ERR_SHARD_NO_DATA"] == oracle.ERR_SHARD_NO_DATA == ia.ErrShardNoData.code
+    assert codes["RSGPU_ERR_SINGULAR"] == oracle.ERR_SINGULAR == ia.ErrSingular.code
+    assert codes["RSGPU_ERR_INV_SHARD_NUM"] == oracle.ERR_INV_SHARD_NUM == ia.ErrInvShardNum.code
+    assert codes["RSGPU_ERR_MAX_SHARD_NUM"] == oracle.ERR_MAX_SHARD_NUM == ia.ErrMaxShardNum.code
+    assert codes["RSGPU_ERR_INVALID_INPUT"] == oracle.ERR_INVALID_INPUT == ia.ErrInvalidInput.code
+    L = _lib.load()
+    for name, code in codes.items():
+        assert L.rsgpu_strerror(code)
+
+
+@pytest.mark.parametrize("kind", ["vandermonde", "cauchy", "par1"])
+@pytest.mark.parametrize("k,p", [(1, 1), (4, 2), (10, 2), (10, 4), (17, 3), (128, 128)])
+def test_matrix_matches_oracle(k, p, kind):
+    enc = ia.New(k, p, matrix=kind)
+    e, want = oracle.build_matrix(k, p, kind)
+    assert e == 0
+    assert np.array_equal(enc.matrix(), want)
+
+
+def test_new_errors():
+    with pytest.raises(ia.ErrInvShardNum):
+        ia.New(0, 2)
+    with pytest.raises(ia.ErrInvShardNum):
+        ia.New(3, 0)
+    with pytest.raises(ia.ErrInvShardNum):
+        ia.New(-1, 2)
+    with pytest.raises(ia.ErrMaxShardNum):
+        ia.New(250, 7)
+    ia.New(250, 6)  # exactly 256 is allowed
+
+
+def test_error_precedence_without_device():
+    """Length and checkShards errors come before any device work."""
+    enc = ia.New(4, 2)
+    with pytest.raises(ia.ErrTooFewShards):
+        enc.Encode([bytearray(8)] * 5)
+    with pytest.raises(ia.ErrShardSize):
+        enc.Encode([bytearray(8)] * 5 + [None])
+    with pytest.raises(ia.ErrShardNoData):
+        enc.Encode([None] * 6)
+    with pytest.raises(ia.ErrShardSize):
+        enc.Verify([bytearray(8)] * 5 + [bytearray(7)])
+    with pytest.raises(ia.ErrTooFewShards):
+        enc.Reconstruct([bytearray(8)] * 3 + [None] * 3)
+    with pytest.raises(ia.ErrTooFewShards):
+        enc.Update([bytearray(8)] * 6, [None] * 3)
+    with pytest.raises(ia.ErrInvalidInput):
+        enc.Update([None] + [bytearray(8)] * 5, [bytearray(8)] + [None] * 3)
+    with pytest.raises(ia.ErrInvalidInput):
+        enc.Update([bytearray(8)] * 5 + [None], [bytearray(8)] + [None] * 3)
+    # all present -> Reconstruct is a no-op (no device needed), as upstream
+    enc.Reconstruct([bytearray(8)] * 6)
+
+
+@pytest.mark.skipif(ia.device_ok(0), reason="only meaningful on a host without the GPU")
+def test_compute_fails_loudly_without_device():
+    enc = ia.New(4, 2)
+    with pytest.raises(ia.NoDevice):
+        enc.Encode([bytearray(8)] * 6)
+    with pytest.raises(ia.NoDevice):
+        enc.Verify([bytearray(8)] * 6)
+    with pytest.raises(ia.NoDevice):
+        enc.Reconstruct([None] + [bytearray(8)] * 5)
+    with pytest.raises(ia.NoDevice):
+        enc.encode_dev(16, 8, 16, 96, 1)
+
+
+def test_device_layout_validation():
+    enc = ia.New(10, 2)
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev(0, 100, 112, 12 * 112, 1)        # NULL base
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev(4096 + 8, 100, 112, 12 * 112, 1)  # misaligned base
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev(4096, 100, 100, 12 * 100, 1)      # pitch % 16
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev(4096, 100, 96, 12 * 96, 1)        # pitch < roundup16(len)
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev(4096, 100, 112, 112, 2)           # objects overlap
+    with pytest.raises(ia.ErrShardNoData):
+        enc.encode_dev(4096, 0, 112, 12 * 112, 1)

@@ -1,0 +1,379 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle, bit-exact.
+
+Small cases compare byte-for-byte with the oracle and the committed golden
+fixtures; BASELINE-size batches (1024 x 1 MiB RS(10+2), 512 x 4 MiB RS(10+4))
+are compared against the oracle's AVX2 port on the same bytes plus
+size-independent properties (encode -> erase -> decode round trip, verify
+flags).  Every test here fails (never skips) without a gfx950 device."""
+import hashlib
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+import infinicache_amd as ia
+import oracle
+from oracle import rs_numpy as rn
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+SEED = 0x1F1C
+
+
+def _data(idx, k, size):
+    return rn.splitmix64_bytes(SEED, idx, k * size).reshape(k, size)
+
+
+def _full(k, p, size, idx=0, kind="vandermonde"):
+    d = _data(idx, k, size)
+    e, sh = oracle.encode(k, p, [d[i] for i in range(k)] + [bytes(size)] * p, kind)
+    assert e == 0
+    return sh
+
+
+# ------------------------------------------------------------- host API
+
+def test_golden_fixtures_host_encode(gpu):
+    g = np.load(os.path.join(GOLDEN, "vectors.npz"))
+    n = 0
+    for key in g.files:
+        if not key.startswith("parity_"):
+            continue
+        _, k, p, kind, size = key.split("_")
+        k, p, size = int(k), int(p), int(size)
+        idx = int(g[f"seedidx_{k}_{p}_{kind}_{size}"][0])
+        d = _data(idx, k, size)
+        enc = ia.New(k, p, matrix=kind)
+        shards = [d[i].copy() for i in range(k)] + [np.zeros(size, np.uint8) for _ in range(p)]
+        enc.Encode(shards)
+        assert np.array_equal(np.stack(shards[k:]), g[key]), key
+        assert enc.Verify(shards), key
+        n += 1
+    assert n >= 40
+
+
+def test_golden_digests_1mib_4mib(gpu):
+    digests = json.load(open(os.path.join(GOLDEN, "digests.json")))
+    for (k, p, nbytes, tag) in [(10, 2, 1 << 20, "rs10_2_1MiB"), (10, 4, 4 << 20, "rs10_4_4MiB")]:
+        enc = ia.New(k, p)
+        for o in range(2):
+            sh = enc.Split(rn.splitmix64_bytes(SEED, o, nbytes))
+            enc.Encode(sh)
+            h = hashlib.sha256(b"".join(s.tobytes() for s in sh[k:])).hexdigest()
+            assert h == digests[f"{tag}_obj{o}"], (tag, o)
+
+
+@pytest.mark.parametrize("size", [1, 2, 15, 16, 17, 103, 255, 4096, 4097, 104858])
+def test_encode_verify_sizes(gpu, size):
+    k, p = 10, 4
+    want = _full(k, p, size, idx=size)
+    enc = ia.New(k, p)
+    sh = [want[i].copy() for i in range(k)] + [np.full(size, 0xAA, np.uint8) for _ in range(p)]
+    enc.Encode(sh)
+    for r in range(k, k + p):
+        assert np.array_equal(sh[r], want[r])
+    assert enc.Verify(sh)
+    for pos in {0, size // 2, size - 1}:  # corruption anywhere, incl. last byte
+        bad = [s.copy() for s in sh]
+        bad[k + p - 1][pos] ^= 0x40
+        assert not enc.Verify(bad)
+        bad = [s.copy() for s in sh]
+        bad[0][pos] ^= 0x01
+        assert not enc.Verify(bad)
+
+
+def test_encode_zero_and_ff(gpu):
+    """log(0) edge: all-zero and all-0xFF objects."""
+    enc = ia.New(10, 2)
+    for fill in (0, 0xFF):
+        sh = [np.full(1000, fill, np.uint8) for _ in range(10)] + [np.zeros(1000, np.uint8)] * 2
+        sh[10] = np.zeros(1000, np.uint8)
+        sh[11] = np.zeros(1000, np.uint8)
+        enc.Encode(sh)
+        e, want = oracle.encode(10, 2, [np.full(1000, fill, np.uint8)] * 10 + [bytes(1000)] * 2)
+        assert np.array_equal(sh[10], want[10]) and np.array_equal(sh[11], want[11])
+
+
+@pytest.mark.parametrize("k,p,kind", [(1, 1, "vandermonde"), (3, 13, "vandermonde"),
+                                      (4, 2, "cauchy"), (6, 3, "par1"), (10, 6, "vandermonde"),
+                                      (16, 4, "vandermonde"), (17, 3, "vandermonde"),
+                                      (20, 4, "cauchy"), (64, 8, "vandermonde")])
+def test_shapes_and_matrix_kinds(gpu, k, p, kind):
+    """K > 16 takes the generic kernel; R > 4 takes several passes."""
+    size = 333
+    want = _full(k, p, size, idx=k * 100 + p, kind=kind)
+    enc = ia.New(k, p, matrix=kind)
+    sh = [want[i].copy() for i in range(k)] + [np.zeros(size, np.uint8) for _ in range(p)]
+    enc.Encode(sh)
+    for r in range(k, k + p):
+        assert np.array_equal(sh[r], want[r]), (k, p, kind, r)
+    assert enc.Verify(sh)
+    # lose min(p, 3) shards spread over data and parity
+    lost = sorted({0, k // 2, k + p - 1}) if p >= 3 else [0, k + p - 1][:p]
+    part = [None if i in lost else sh[i].copy() for i in range(k + p)]
+    if kind == "par1":
+        try:
+            enc.Reconstruct(part)
+        except ia.ErrSingular:  # PAR1 is not MDS; upstream may fail too
+            e, _ = oracle.reconstruct(k, p, [None if i in lost else sh[i] for i in range(k + p)], kind)
+            assert e == oracle.ERR_SINGULAR
+            return
+    else:
+        enc.Reconstruct(part)
+    for i in range(k + p):
+        assert np.array_equal(part[i], want[i]), (k, p, kind, i)
+
+
+def test_reconstruct_all_patterns_rs10_2(gpu):
+    k, p, size = 10, 2, 1031
+    full = _full(k, p, size, idx=7)
+    enc = ia.New(k, p)
+    for ne in (1, 2):
+        for lost in itertools.combinations(range(k + p), ne):
+            sh = [None if i in lost else full[i].copy() for i in range(k + p)]
+            enc.Reconstruct(sh)
+            for i in range(k + p):
+                assert np.array_equal(sh[i], full[i]), (lost, i)
+
+
+def test_reconstruct_data_only_rs10_4_all_2data(gpu):
+    k, p, size = 10, 4, 999
+    full = _full(k, p, size, idx=8)
+    enc = ia.New(k, p)
+    for lost in itertools.combinations(range(k), 2):
+        lost = set(lost) | {12}
+        sh = [None if i in lost else full[i].copy() for i in range(k + p)]
+        enc.ReconstructData(sh)
+        for i in range(k):
+            assert np.array_equal(sh[i], full[i]), (lost, i)
+        assert sh[12] is None  # parity left missing, as upstream
+
+
+def test_reconstruct_matches_oracle_on_corrupt_input(gpu):
+    """With inconsistent shards the output depends on WHICH survivors are
+    used; upstream uses the first k present in index order."""
+    k, p, size = 10, 4, 257
+    full = _full(k, p, size, idx=9)
+    bad = [s.copy() for s in full]
+    bad[11][3] ^= 0x5A
+    bad[13][100] ^= 0x01
+    for lost in [(0, 1), (2, 12), (5,)]:
+        sh = [None if i in lost else bad[i].copy() for i in range(k + p)]
+        e, want = oracle.reconstruct(k, p, sh)
+        assert e == 0
+        ia.New(k, p).Reconstruct(sh)
+        for i in range(k + p):
+            assert np.array_equal(sh[i], want[i]), (lost, i)
+
+
+def test_decode_verify_fused(gpu):
+    """Client.decode = Verify -> Reconstruct -> Verify (ecRedis.go:404-427)."""
+    k, p, size = 10, 2, 4000
+    full = _full(k, p, size, idx=10)
+    enc = ia.New(k, p)
+    # healthy Get: exactly k bodies (proxy first-d rule) -> always consistent
+    sh = [None if i in (3, 8) else full[i].copy() for i in range(k + p)]
+    assert enc.DecodeVerify(sh)
+    assert all(np.array_equal(sh[i], full[i]) for i in range(k + p))
+    # 11 present, one missing: the extra parity shard is really checked
+    sh = [None if i == 4 else full[i].copy() for i in range(k + p)]
+    assert enc.DecodeVerify(sh)
+    sh = [None if i == 4 else full[i].copy() for i in range(k + p)]
+    sh[11][size - 1] ^= 1
+    e, want = oracle.reconstruct(k, p, sh)
+    ok = enc.DecodeVerify(sh)
+    e2, ok2 = oracle.verify(k, p, want)
+    assert ok == ok2 == False  # noqa: E712
+    assert np.array_equal(sh[4], want[4])
+    # all present: plain Verify
+    assert enc.DecodeVerify([s.copy() for s in full])
+    bad = [s.copy() for s in full]
+    bad[10][0] ^= 2
+    assert not enc.DecodeVerify(bad)
+
+
+def test_update_matches_oracle(gpu):
+    k, p, size = 10, 4, 777
+    full = _full(k, p, size, idx=11)
+    rng = np.random.default_rng(5)
+    new = [None] * k
+    for c in (0, 3, 9):
+        new[c] = rng.integers(0, 256, size, dtype=np.uint8)
+    e, want = oracle.update(k, p, full, new)
+    sh = [s.copy() for s in full]
+    ia.New(k, p).Update(sh, new)
+    for i in range(k + p):
+        assert np.array_equal(sh[i], want[i]), i
+
+
+def test_concurrent_host_calls(gpu):
+    """Encoders are safe for concurrent use (upstream contract)."""
+    from concurrent.futures import ThreadPoolExecutor
+    enc = ia.New(10, 2)
+    objs = [_full(10, 2, 5000 + 13 * i, idx=100 + i) for i in range(16)]
+
+    def job(i):
+        w = objs[i]
+        sh = [w[c].copy() for c in range(10)] + [np.zeros(len(w[0]), np.uint8) for _ in range(2)]
+        enc.Encode(sh)
+        lost = [None if c in (i % 12, (i + 5) % 12) else sh[c] for c in range(12)]
+        enc.Reconstruct(lost)
+        return all(np.array_equal(lost[c], w[c]) for c in range(12))
+
+    with ThreadPoolExecutor(8) as ex:
+        assert all(ex.map(job, range(16)))
+
+
+# ------------------------------------------------- device-resident batch API
+
+torch = pytest.importorskip("torch")
+
+
+def _dev_batch(nobj, n, S, pitch, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    b = torch.randint(0, 256, (nobj, n, pitch), dtype=torch.uint8, device="cuda", generator=g)
+    b[:, :, S:] = 0
+    return b
+
+
+@pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 1, 3), (10, 2, 4099, 7), (10, 4, 70000, 5),
+                                        (17, 3, 1000, 4), (10, 6, 2000, 2)])
+def test_dev_encode_small_vs_oracle(gpu, k, p, S, nobj):
+    pitch = (S + 255) // 256 * 256
+    b = _dev_batch(nobj, k + p, S, pitch, seed=S)
+    enc = ia.New(k, p)
+    enc.encode_dev(b, S, pitch, (k + p) * pitch, nobj, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    h = b.cpu().numpy()
+    m = enc.matrix()
+    for o in range(nobj):
+        want = oracle.apply(m[k:], [h[o, c, :S] for c in range(k)])
+        for r in range(p):
+            assert np.array_equal(h[o, k + r, :S], want[r]), (o, r)
+
+
+def test_dev_rs10_2_1mib_batch1024_encode_decode(gpu):
+    """BASELINE config 2 + the north-star encode+decode step at full size."""
+    k, p, S, nobj = 10, 2, 104858, 1024
+    pitch = (S + 255) // 256 * 256
+    stride = (k + p) * pitch
+    b = _dev_batch(nobj, k + p, S, pitch, seed=1234)
+    orig_data = b[:, :k].clone()
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    torch.cuda.synchronize()
+    h = b.cpu().numpy()
+    # bit-exact vs the oracle's AVX2 port over the whole batch
+    ref = h.copy()
+    ref[:, k:, :] = 0
+    m = enc.matrix()
+    oracle.code_batch(m[k:], list(range(k)), list(range(k, k + p)), ref.reshape(-1), stride, pitch,
+                      S, nobj, nthreads=16)
+    assert np.array_equal(h[:, :, :S], ref[:, :, :S])
+    bad = torch.ones(nobj, dtype=torch.int32, device="cuda")
+    enc.verify_dev(b, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert int(bad.sum()) == 0
+    # erase data shards {0, 5} on every object, fused decode, compare
+    present = [i not in (0, 5) for i in range(k + p)]
+    b[:, 0].fill_(0x33)
+    b[:, 5].fill_(0x77)
+    enc.decode_dev(b, present, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert int(bad.sum()) == 0
+    assert torch.equal(b[:, :k, :S], orig_data[:, :, :S])
+
+
+def test_dev_rs10_4_4mib_decode_all_2data_patterns(gpu):
+    """BASELINE config 3: RS(10+4) decode with 2 missing data shards, 4 MiB
+    objects; every C(10,2) pattern on a small batch, {0,5} at batch 512."""
+    k, p, S = 10, 4, 419431
+    pitch = (S + 255) // 256 * 256
+    stride = (k + p) * pitch
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    nobj = 4
+    b = _dev_batch(nobj, k + p, S, pitch, seed=99)
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    golden = b.clone()
+    for lost in itertools.combinations(range(k), 2):
+        present = [i not in lost for i in range(k + p)]
+        for i in lost:
+            b[:, i].fill_(0)
+        enc.reconstruct_dev(b, present, S, pitch, stride, nobj, data_only=True, stream=s)
+        torch.cuda.synchronize()
+        assert torch.equal(b[:, :, :S], golden[:, :, :S]), lost
+    nobj = 512
+    b = _dev_batch(nobj, k + p, S, pitch, seed=100)
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    golden = b[:, :k].clone()
+    b[:, 0].fill_(1)
+    b[:, 5].fill_(2)
+    present = [i not in (0, 5) for i in range(k + p)]
+    enc.reconstruct_dev(b, present, S, pitch, stride, nobj, data_only=True, stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(b[:, :k, :S], golden[:, :, :S])
+    # parity vs oracle on a few objects of the big batch
+    h = b[:3].cpu().numpy()
+    m = enc.matrix()
+    for o in range(3):
+        want = oracle.code_fast(m[k:], [h[o, c, :S] for c in range(k)], nthreads=8)
+        for r in range(p):
+            assert np.array_equal(h[o, k + r, :S], want[r])
+
+
+def test_dev_verify_flags_per_object(gpu):
+    k, p, S, nobj = 10, 2, 5001, 9
+    pitch = 5120
+    stride = (k + p) * pitch
+    b = _dev_batch(nobj, k + p, S, pitch, seed=3)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    b[2, 11, S - 1] ^= 1     # last valid byte of parity
+    b[5, 0, 0] ^= 0x80       # first data byte
+    b[7, 3, S] = 9           # pad byte: must NOT count
+    bad = torch.full((nobj,), 7, dtype=torch.int32, device="cuda")
+    enc.verify_dev(b, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert bad.cpu().tolist() == [0, 0, 1, 0, 0, 1, 0, 0, 0]
+
+
+def test_dev_decode_with_extra_checks(gpu):
+    k, p, S, nobj = 10, 4, 3000, 6
+    pitch = 3072
+    stride = (k + p) * pitch
+    b = _dev_batch(nobj, k + p, S, pitch, seed=4)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    golden = b.clone()
+    b[4, 13, 17] ^= 0xFF  # corrupt an extra (non-survivor) parity shard
+    present = [i not in (1, 2) for i in range(k + p)]  # 12 present: 2 extras
+    b[:, 1].zero_()
+    b[:, 2].zero_()
+    bad = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+    enc.decode_dev(b, present, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert bad.cpu().tolist() == [0, 0, 0, 0, 1, 0]
+    assert torch.equal(b[:, :k, :S], golden[:, :k, :S])
+
+
+def test_dev_many_objects_grid_y_split(gpu):
+    """nobj > 65535 exercises the grid.y batching in the launcher."""
+    k, p, S, nobj = 4, 2, 16, 70000
+    pitch = 16
+    stride = (k + p) * pitch
+    b = _dev_batch(nobj, k + p, S, pitch, seed=5)
+    enc = ia.New(k, p)
+    enc.encode_dev(b, S, pitch, stride, nobj, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    h = b.cpu().numpy()
+    m = enc.matrix()
+    for o in (0, 65534, 65535, 69999):
+        want = oracle.apply(m[k:], [h[o, c] for c in range(k)])
+        for r in range(p):
+            assert np.array_equal(h[o, k + r], want[r]), o

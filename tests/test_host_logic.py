@@ -1,0 +1,87 @@
+"""Host-side mirror semantics that run without a GPU: Split / Join (upstream
+Join = /root/reference/client/ec.go:83-121), DummyEncoder
+(/root/reference/client/ec.go:26-121) and NewEncoder (ec.go:14-24)."""
+import io
+
+import numpy as np
+import pytest
+
+import infinicache_amd as ia
+from oracle import rs_numpy as rn
+
+
+def test_split_pads_to_k_plus_p_one_backing_array():
+    enc = ia.New(10, 2)
+    data = bytes(range(256)) * 4 + b"xyz"  # 1027 bytes
+    sh = enc.Split(data)
+    assert len(sh) == 12 and all(len(s) == 103 for s in sh)
+    assert sh[0].base is sh[11].base  # one backing array, as upstream
+    assert np.concatenate(sh).tobytes()[:1027] == data
+    assert not np.concatenate(sh)[1027:].any()
+    for a, b in zip(sh, rn.split(data, 10, 2)):
+        assert np.array_equal(a, b)
+
+
+def test_split_short_data():
+    with pytest.raises(ia.ErrShortData):
+        ia.New(10, 2).Split(b"")
+
+
+def test_split_one_byte():
+    sh = ia.New(10, 2).Split(b"\x07")
+    assert [len(s) for s in sh] == [1] * 12 and sh[0][0] == 7
+
+
+def test_join_roundtrip_and_errors():
+    enc = ia.New(4, 2)
+    data = b"0123456789abcdefXYZ"
+    sh = enc.Split(data)
+    out = io.BytesIO()
+    enc.Join(out, sh, len(data))
+    assert out.getvalue() == data
+    out = io.BytesIO()
+    enc.Join(out, sh, 5)
+    assert out.getvalue() == data[:5]
+    with pytest.raises(ia.ErrTooFewShards):
+        enc.Join(io.BytesIO(), sh[:3], len(data))
+    bad = list(sh)
+    bad[1] = None
+    with pytest.raises(ia.ErrReconstructRequired):
+        enc.Join(io.BytesIO(), bad, len(data))
+    with pytest.raises(ia.ErrShortData):
+        enc.Join(io.BytesIO(), sh, 4 * len(sh[0]) + 1)
+    # parity shards missing is fine: Join reads data shards only
+    nopar = list(sh[:4]) + [None, None]
+    out = io.BytesIO()
+    enc.Join(out, nopar, len(data))
+    assert out.getvalue() == data
+
+
+def test_dummy_encoder_semantics():
+    d = ia.DummyEncoder(4)
+    sh = d.Split(b"0123456789")  # perShard 3: 3,3,3,1 — no padding
+    assert [bytes(s) for s in sh] == [b"012", b"345", b"678", b"9"]
+    assert d.Verify(sh)
+    with pytest.raises(ia.ErrTooFewShards):
+        d.Verify(sh[:3])
+    with pytest.raises(ia.ErrTooFewShards):
+        d.Verify(sh[:3] + [b""])
+    with pytest.raises(ia.ErrNotImplemented):
+        d.Update(sh, sh)
+    assert d.Encode(sh) is None
+    out = io.BytesIO()
+    d.Join(out, sh, 10)
+    assert out.getvalue() == b"0123456789"
+    with pytest.raises(ia.ErrShortData):
+        d.Split(b"")
+    # fewer bytes than shards: ec.go:77-79 stores the empty remainder in the
+    # next shard (a non-nil empty slice); later shards stay nil
+    sh = d.Split(b"ab")
+    assert [None if s is None else bytes(s) for s in sh] == [b"a", b"b", b"", None]
+
+
+def test_new_encoder_factory(capsys):
+    assert isinstance(ia.NewEncoder(10, 0, 32), ia.DummyEncoder)
+    assert isinstance(ia.NewEncoder(10, 2, 32), ia.RSEncoder)
+    assert ia.NewEncoder(0, 2, 32) is None  # error printed and swallowed
+    assert "newEncoder err" in capsys.readouterr().out
