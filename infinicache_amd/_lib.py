@@ -46,6 +46,16 @@ def load():
         raise LibraryMissing(
             f"{LIB_PATH} not found: build it with `make -C infinicache_amd/csrc` "
             "(or python -c 'import __graft_entry__ as g; g.build()')")
+    # One HIP runtime per process: PyTorch-ROCm wheels bundle their own
+    # libamdhip64.so.7 (+ HSA runtime).  If torch is installed it is imported
+    # first so librsgpu.so's NEEDED libamdhip64.so.7 binds to that already
+    # loaded runtime (same SONAME); otherwise a second runtime initialised
+    # before torch makes torch see no device.  Without torch (a C/Go host)
+    # the library uses /opt/rocm's runtime via its RUNPATH.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     L.rsgpu_create.argtypes = [ci, ci, ci, ctypes.c_uint, ctypes.POINTER(vp)]
     L.rsgpu_destroy.argtypes = [vp]

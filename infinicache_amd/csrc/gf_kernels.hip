@@ -22,12 +22,19 @@
 
 #include "gf_apply.h"
 #include "gf256.h"
+#include "gf_device.h"
 
 namespace rsgpu {
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kBlock = 256;
+// Tuned launch shape of the specialised pass (tools/kbench.hip sweep on
+// MI355X): 256 lanes x one 16-B vector per row;
+// non-temporal (nt) input loads — every input byte is read exactly once, so
+// keeping it out of the caches frees them for the output write stream
+// (59% -> 75% of HBM peak); stores with sc0|sc1 (+2.5 points).
+constexpr int kBlock = 256;    // lanes per workgroup
+constexpr int kUnroll = 1;     // 16-B vectors per lane
+constexpr int kLoadAux = 2;    // buffer_load: nt
+constexpr int kStoreAux = 17;  // buffer_store: sc0 | sc1
 constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
 constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
@@ -51,98 +58,6 @@ Plan::~Plan() {
     if (d_in_row) (void)hipFree(d_in_row);
 }
 
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ uint32_t lut(uint32_t t, uint32_t sel) {
-    return __builtin_amdgcn_perm(t, t, sel);
-}
-
-// acc ^= c (x) w, for one dword w whose 2-bit group indices are i0..i3.
-__device__ __forceinline__ uint32_t gf_mac(uint32_t acc, const uint32_t *t, uint32_t i0,
-                                           uint32_t i1, uint32_t i2, uint32_t i3) {
-    acc = xor3(acc, lut(t[0], i0), lut(t[1], i1));
-    return xor3(acc, lut(t[2], i2), lut(t[3], i3));
-}
-
-// mask of the valid bytes of dword d in a 16-B vector holding `valid` bytes
-__device__ __forceinline__ uint32_t tail_mask(int d, uint32_t valid) {
-    int v = (int)valid - 4 * d;
-    if (v >= 4) return 0xffffffffu;
-    if (v <= 0) return 0u;
-    return (1u << (8 * v)) - 1u;
-}
-
-template <int K, int R>
-struct ApplyArgs {
-    const uint8_t *base;
-    uint64_t obj_stride;
-    uint32_t *bad;
-    uint32_t nvec;  // 16-B vectors per row
-    uint32_t tail;  // valid bytes in the last vector (1..16)
-    uint32_t nw;
-    uint32_t span;  // bytes addressable from an object base
-    uint32_t in_off[K];
-    uint32_t out_off[R];
-    uint32_t tab[K * R * 4];  // input-major [K][R][4]: one s_load_dwordx(4R) per input
-};
-
-template <int K, int R>
-__global__ __launch_bounds__(kBlock) void gf_apply_kernel(const ApplyArgs<K, R> a) {
-    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
-    if (v >= a.nvec) return;
-    const uint8_t *ob = a.base + (uint64_t)blockIdx.y * a.obj_stride;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
-    const uint32_t voff = v * 16u;
-
-    u32x4 x[K];
-#pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_off[c], 0);
-
-    uint32_t acc[R][4];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) acc[r][d] = 0;
-
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const uint32_t w = x[c][d];
-            const uint32_t i0 = w & 0x03030303u;
-            const uint32_t i1 = (w >> 2) & 0x03030303u;
-            const uint32_t i2 = (w >> 4) & 0x03030303u;
-            const uint32_t i3 = (w >> 6) & 0x03030303u;
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], &a.tab[(c * R + r) * 4], i0, i1, i2, i3);
-        }
-        // keep the input-at-a-time order: without these fences the IR
-        // passes and the scheduler hoist every input's index math and split
-        // the work row by row (160+ VGPRs, 2 waves/SIMD)
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
-        __builtin_amdgcn_sched_barrier(0);
-    }
-
-    bool mismatch = false;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if ((uint32_t)r < a.nw) {
-            u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-            __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, a.out_off[r], 0);
-        } else {
-            const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
-        }
-    }
-    if (mismatch) atomicOr(a.bad + blockIdx.y, 1u);
-}
-
 // Generic pass for K > 16 inputs (any shard count up to 256): runtime input
 // loop, tables read by scalar loads from a device buffer laid out [K][R][4].
 struct GenericArgs {
@@ -151,7 +66,7 @@ struct GenericArgs {
     uint32_t *bad;
     const uint32_t *tab;     // [K][rstride][4], pre-offset to this pass's first row
     const uint32_t *in_row;  // [K] row indices; offset = row * pitch
-    uint32_t nvec, tail, nw, span, K, rstride, pitch;
+    uint32_t nvec, tail, nw, span, K, rstride, pitch, clear;
     uint32_t out_off[kMaxR];
 };
 
@@ -169,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
 #pragma unroll
         for (int d = 0; d < 4; ++d) acc[r][d] = 0;
     for (uint32_t c = 0; c < a.K; ++c) {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_row[c] * a.pitch, 0);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_row[c] * a.pitch, kLoadAux);
         const uint32_t *t = a.tab + (size_t)c * a.rstride * 4;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -187,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     for (int r = 0; r < R; ++r) {
         if ((uint32_t)r < a.nw) {
             u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-            __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, a.out_off[r], 0);
+            __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, a.out_off[r], kStoreAux);
         } else {
             const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
 #pragma unroll
@@ -195,6 +110,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
         }
     }
     if (mismatch) atomicOr(a.bad + blockIdx.y, 1u);
+    if (a.clear && v == 0) a.bad[blockIdx.y] = 0u;
 }
 
 // ----------------------------------------------------------------- launchers
@@ -229,12 +145,14 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
                 a.tab[(c * R + r) * 4 + g] = p.tab[((size_t)(s.r0 + r) * K + c) * 4 + g];
     }
     a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * 16);
-    const unsigned gx = (a.nvec + kBlock - 1) / kBlock;
+    const unsigned gx = (a.nvec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
     for (int o0 = 0; o0 < L.nobj; o0 += kMaxGridY) {
         const int no = std::min(kMaxGridY, L.nobj - o0);
         a.base = L.base + (size_t)o0 * L.obj_stride;
         a.bad = d_bad ? d_bad + o0 : nullptr;
-        hipLaunchKernelGGL((gf_apply_kernel<K, R>), dim3(gx, no), dim3(kBlock), 0, st, a);
+        a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
+        hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(gx, no),
+                           dim3(kBlock), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -285,6 +203,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         const int no = std::min(kMaxGridY, L.nobj - o0);
         a.base = L.base + (size_t)o0 * L.obj_stride;
         a.bad = d_bad ? d_bad + o0 : nullptr;
+        a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
         hipLaunchKernelGGL((gf_apply_generic<R>), dim3(gx, no), dim3(kBlock), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -626,8 +626,11 @@ static int recon_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_
     std::shared_ptr<Plan> plan;
     if ((e = ctx->plan_reconstruct(present, data_only, check, plan))) return e;
     Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
-    if (check) HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
-    HIP_TRY(launch_plan(*plan, L, d_bad, (hipStream_t)stream));
+    // with check rows the flags are OR-ed by the kernel and need a memset
+    // first; without, the kernel clears them itself (no extra launch)
+    if (check && plan->nw < plan->R)
+        HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
+    HIP_TRY(launch_plan(*plan, L, check ? d_bad : nullptr, (hipStream_t)stream));
     return RSGPU_OK;
 }
 

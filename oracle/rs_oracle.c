@@ -20,8 +20,11 @@
  *
  * Two kernels are provided:
  *   - scalar table-driven coding (the "galMulSlice(Xor)" generic Go path);
- *   - an AVX2 PSHUFB nibble-table coder + codeSomeShardsP byte-range split on
- *     pthreads: the CPU baseline bench.py times (cpu_baseline.kind = "port").
+ *   - the upstream SIMD coders restated: AVX2 PSHUFB nibble tables
+ *     (galMulAVX2/galMulAVX2Xor) and the AVX-512 multi-output form
+ *     (codeSomeShardsAvx512), with the codeSomeShardsP byte-range split on a
+ *     persistent thread pool: the CPU baseline bench.py times
+ *     (cpu_baseline.kind = "port").
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -359,10 +362,56 @@ static void gal_mul_avx2(uint8_t c, const uint8_t *in, uint8_t *out, size_t n, i
 }
 #endif
 
+#if defined(__x86_64__)
+/* upstream codeSomeShardsAvx512 (galMulAVX512Parallel82/84, used when the CPU
+ * has AVX512F+BW, >= 4 inputs and >= 2 outputs): each 64-B block of every
+ * input is read once and multiplied into up to 4 output accumulators held in
+ * zmm registers (low/high-nibble VPSHUFB tables, as galMulAVX2). */
+__attribute__((target("avx512f,avx512bw")))
+static void code_range_avx512(const uint8_t *const *rows, int nrows, const uint8_t *const *inputs,
+                              int ninputs, uint8_t *const *outputs, size_t start, size_t stop) {
+    const __m512i mask = _mm512_set1_epi8(0x0f);
+    for (int r0 = 0; r0 < nrows; r0 += 4) {
+        const int nr = nrows - r0 < 4 ? nrows - r0 : 4;
+        size_t i = start;
+        for (; i + 64 <= stop; i += 64) {
+            __m512i acc[4] = {_mm512_setzero_si512(), _mm512_setzero_si512(),
+                              _mm512_setzero_si512(), _mm512_setzero_si512()};
+            for (int c = 0; c < ninputs; c++) {
+                const __m512i x = _mm512_loadu_si512((const void *)(inputs[c] + i));
+                const __m512i lo = _mm512_and_si512(x, mask);
+                const __m512i hi = _mm512_and_si512(_mm512_srli_epi64(x, 4), mask);
+                for (int r = 0; r < nr; r++) {
+                    const uint8_t cf = rows[r0 + r][c];
+                    const __m512i tl = _mm512_broadcast_i32x4(_mm_loadu_si128((const __m128i *)MUL_LO[cf]));
+                    const __m512i th = _mm512_broadcast_i32x4(_mm_loadu_si128((const __m128i *)MUL_HI[cf]));
+                    acc[r] = _mm512_ternarylogic_epi64(acc[r], _mm512_shuffle_epi8(tl, lo),
+                                                       _mm512_shuffle_epi8(th, hi), 0x96);
+                }
+            }
+            for (int r = 0; r < nr; r++) _mm512_storeu_si512((void *)(outputs[r0 + r] + i), acc[r]);
+        }
+        if (i < stop) {  /* < 64 B tail: generic table loop, as upstream */
+            const uint8_t *rr[4];
+            for (int r = 0; r < nr; r++) rr[r] = rows[r0 + r];
+            code_scalar(rr, nr, inputs, ninputs, outputs + r0, i, stop);
+        }
+    }
+}
+#endif
+
 static void code_range_fast(const uint8_t *const *rows, int nrows, const uint8_t *const *inputs,
                             int ninputs, uint8_t *const *outputs, size_t start, size_t stop) {
 #if defined(__x86_64__)
-    if (__builtin_cpu_supports("avx2")) {
+    static int isa = -1;
+    if (isa < 0)
+        isa = (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw")) ? 2
+              : __builtin_cpu_supports("avx2") ? 1 : 0;
+    if (isa == 2 && ninputs >= 4 && nrows >= 2 && !getenv("ORC_NO_AVX512")) {
+        code_range_avx512(rows, nrows, inputs, ninputs, outputs, start, stop);
+        return;
+    }
+    if (isa >= 1) {
         for (int c = 0; c < ninputs; c++)
             for (int r = 0; r < nrows; r++)
                 gal_mul_avx2(rows[r][c], inputs[c] + start, outputs[r] + start, stop - start, c != 0);
@@ -372,29 +421,113 @@ static void code_range_fast(const uint8_t *const *rows, int nrows, const uint8_t
     code_scalar(rows, nrows, inputs, ninputs, outputs, start, stop);
 }
 
+/* ISA the fast coder uses on this host: "avx512bw", "avx2" or "scalar". */
+const char *orc_cpu_isa(void) {
+#if defined(__x86_64__)
+    if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") && !getenv("ORC_NO_AVX512"))
+        return "avx512bw";
+    if (__builtin_cpu_supports("avx2")) return "avx2";
+#endif
+    return "scalar";
+}
+
+/* ---- persistent worker pool (goroutine stand-in): workers spin briefly,
+ * then sleep on a condvar; the submitting thread participates. */
+typedef struct {
+    void (*fn)(void *, int);
+    void *arg;
+    int ntasks;
+    int next, done;   /* atomics */
+    int active;       /* workers inside run_tasks (guarded by POOL.mu) */
+} task_t;
+
+static struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int nthreads;
+    unsigned long gen;
+    task_t *task;
+    pthread_mutex_t submit;   /* one job at a time */
+} POOL = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0, NULL, PTHREAD_MUTEX_INITIALIZER};
+
+static void run_tasks(task_t *t) {
+    for (;;) {
+        int i = __atomic_fetch_add(&t->next, 1, __ATOMIC_ACQ_REL);
+        if (i >= t->ntasks) break;
+        t->fn(t->arg, i);
+        __atomic_fetch_add(&t->done, 1, __ATOMIC_ACQ_REL);
+    }
+}
+
+static void *pool_worker(void *unused) {
+    (void)unused;
+    unsigned long seen = 0;
+    for (;;) {
+        task_t *t = NULL;
+        for (int spin = 0; spin < 20000; spin++) {
+            if (__atomic_load_n(&POOL.gen, __ATOMIC_ACQUIRE) != seen) break;
+            __builtin_ia32_pause();
+        }
+        pthread_mutex_lock(&POOL.mu);
+        while (POOL.gen == seen) pthread_cond_wait(&POOL.cv, &POOL.mu);
+        seen = POOL.gen;
+        t = POOL.task;
+        if (t) t->active++;
+        pthread_mutex_unlock(&POOL.mu);
+        if (t) {
+            run_tasks(t);
+            pthread_mutex_lock(&POOL.mu);
+            t->active--;
+            pthread_cond_broadcast(&POOL.cv);
+            pthread_mutex_unlock(&POOL.mu);
+        }
+    }
+    return NULL;
+}
+
+static void pool_run(void (*fn)(void *, int), void *arg, int ntasks, int nthreads) {
+    if (nthreads <= 1 || ntasks <= 1) {
+        for (int i = 0; i < ntasks; i++) fn(arg, i);
+        return;
+    }
+    pthread_mutex_lock(&POOL.submit);
+    pthread_mutex_lock(&POOL.mu);
+    while (POOL.nthreads < nthreads - 1 && POOL.nthreads < 255) {
+        pthread_t th;
+        pthread_create(&th, NULL, pool_worker, NULL);
+        pthread_detach(th);
+        POOL.nthreads++;
+    }
+    task_t t = {fn, arg, ntasks, 0, 0, 0};
+    POOL.task = &t;
+    __atomic_add_fetch(&POOL.gen, 1, __ATOMIC_RELEASE);
+    pthread_cond_broadcast(&POOL.cv);
+    pthread_mutex_unlock(&POOL.mu);
+    run_tasks(&t);
+    while (__atomic_load_n(&t.done, __ATOMIC_ACQUIRE) < ntasks) __builtin_ia32_pause();
+    pthread_mutex_lock(&POOL.mu);
+    POOL.task = NULL;   /* late wakers see no job */
+    while (t.active > 0) pthread_cond_wait(&POOL.cv, &POOL.mu);  /* t lives on this stack */
+    pthread_mutex_unlock(&POOL.mu);
+    pthread_mutex_unlock(&POOL.submit);
+}
+
 typedef struct {
     const uint8_t *const *rows; int nrows;
     const uint8_t *const *inputs; int ninputs;
     uint8_t *const *outputs;
     size_t len, chunk;
-    int next;          /* next range index, atomic */
-    int nranges;
 } job_t;
 
-static void *worker(void *arg) {
+static void range_task(void *arg, int idx) {
     job_t *j = (job_t *)arg;
-    for (;;) {
-        int idx = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
-        if (idx >= j->nranges) break;
-        size_t s = (size_t)idx * j->chunk, e = s + j->chunk;
-        if (e > j->len) e = j->len;
-        code_range_fast(j->rows, j->nrows, j->inputs, j->ninputs, j->outputs, s, e);
-    }
-    return NULL;
+    size_t s = (size_t)idx * j->chunk, e = s + j->chunk;
+    if (e > j->len) e = j->len;
+    code_range_fast(j->rows, j->nrows, j->inputs, j->ninputs, j->outputs, s, e);
 }
 
-/* codeSomeShardsP on `nthreads` OS threads, maxGoroutines = max_g,
- * minSplitSize = 1024 (upstream defaults).  nthreads <= 1 runs inline. */
+/* codeSomeShardsP: byte ranges of do = max(len/maxGoroutines, minSplitSize
+ * = 1024) rounded up to 64 B, run on `nthreads` pool threads. */
 void orc_code_fast(const uint8_t *coef, int nrows, int ninputs, const uint8_t *const *inputs,
                    uint8_t *const *outputs, size_t len, int nthreads, int max_g) {
     gf_init();
@@ -404,53 +537,36 @@ void orc_code_fast(const uint8_t *coef, int nrows, int ninputs, const uint8_t *c
     size_t chunk = len / (size_t)max_g;
     if (chunk < 1024) chunk = 1024;
     chunk = (chunk + 63) & ~(size_t)63;
-    job_t j = {rows, nrows, inputs, ninputs, outputs, len, chunk, 0, (int)((len + chunk - 1) / chunk)};
-    if (nthreads <= 1 || j.nranges <= 1) { worker(&j); return; }
-    int nt = nthreads < j.nranges ? nthreads : j.nranges;
-    pthread_t th[256];
-    if (nt > 256) nt = 256;
-    for (int t = 1; t < nt; t++) pthread_create(&th[t], NULL, worker, &j);
-    worker(&j);
-    for (int t = 1; t < nt; t++) pthread_join(th[t], NULL);
+    job_t j = {rows, nrows, inputs, ninputs, outputs, len, chunk};
+    pool_run(range_task, &j, (int)((len + chunk - 1) / chunk), nthreads);
 }
 
-/* Batch CPU baseline: for each object o, apply coef to inputs at
- * base + o*obj_stride + in_rows[c]*pitch, writing out_rows[r].  Objects are
- * distributed over `nthreads` threads (one object per task), and within a task
- * the AVX2 coder runs single-threaded — the throughput form of the Go path
- * for many concurrent EcSet/EcGet calls. */
+/* Batch job: object o's inputs at base + o*obj_stride + in_rows[c]*pitch,
+ * outputs at out_rows[r]. */
 typedef struct {
     const uint8_t *coef; int nrows, ninputs;
     const int *in_rows, *out_rows;
     uint8_t *base; size_t obj_stride, pitch, len;
-    int nobj, next;
 } bjob_t;
 
-static void *bworker(void *arg) {
+static void obj_task(void *arg, int o) {
     bjob_t *j = (bjob_t *)arg;
     const uint8_t *rows[256], *ins[256];
     uint8_t *outs[256];
     for (int r = 0; r < j->nrows; r++) rows[r] = j->coef + (size_t)r * j->ninputs;
-    for (;;) {
-        int o = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
-        if (o >= j->nobj) break;
-        uint8_t *ob = j->base + (size_t)o * j->obj_stride;
-        for (int c = 0; c < j->ninputs; c++) ins[c] = ob + (size_t)j->in_rows[c] * j->pitch;
-        for (int r = 0; r < j->nrows; r++) outs[r] = ob + (size_t)j->out_rows[r] * j->pitch;
-        code_range_fast(rows, j->nrows, ins, j->ninputs, outs, 0, j->len);
-    }
-    return NULL;
+    uint8_t *ob = j->base + (size_t)o * j->obj_stride;
+    for (int c = 0; c < j->ninputs; c++) ins[c] = ob + (size_t)j->in_rows[c] * j->pitch;
+    for (int r = 0; r < j->nrows; r++) outs[r] = ob + (size_t)j->out_rows[r] * j->pitch;
+    code_range_fast(rows, j->nrows, ins, j->ninputs, outs, 0, j->len);
 }
 
+/* Batch CPU baseline, object-parallel: one object per task on `nthreads`
+ * pool threads, the fast coder single-threaded inside a task (the throughput
+ * form of many concurrent EcSet/EcGet calls). */
 void orc_code_batch(const uint8_t *coef, int nrows, int ninputs, const int *in_rows,
                     const int *out_rows, uint8_t *base, size_t obj_stride, size_t pitch,
                     size_t len, int nobj, int nthreads) {
     gf_init();
-    bjob_t j = {coef, nrows, ninputs, in_rows, out_rows, base, obj_stride, pitch, len, nobj, 0};
-    if (nthreads <= 1) { bworker(&j); return; }
-    pthread_t th[256];
-    int nt = nthreads > 256 ? 256 : nthreads;
-    for (int t = 1; t < nt; t++) pthread_create(&th[t], NULL, bworker, &j);
-    bworker(&j);
-    for (int t = 1; t < nt; t++) pthread_join(th[t], NULL);
+    bjob_t j = {coef, nrows, ninputs, in_rows, out_rows, base, obj_stride, pitch, len};
+    pool_run(obj_task, &j, nobj, nthreads);
 }

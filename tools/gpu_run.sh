@@ -1,0 +1,36 @@
+#!/bin/bash
+# One gpurun session: GPU parity tests, smoke, bench, rocprofv3 kernel trace.
+# Each GPU step has its own time limit; the script stops at the first crash
+# (abort/segfault/timeout) and never retries a GPU step.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+crashed() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() {  # run <name> <timeout> cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if crashed $rc; then echo "CRASH in $name; stopping"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"pytest smoke bench prof"}
+for s in $STEPS; do
+  case $s in
+    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  run bench 600 python bench.py ;;
+    bench_all)
+            run bench_enc 300 python bench.py --workload enc --no-cpu
+            run bench_dec4 300 python bench.py --workload dec4 --no-cpu ;;
+    kbench) run kbench 300 ./tools/kbench 30 ;;
+    kbench) run kbench 300 ./tools/kbench 30 ;;
+    cpuinfo) (nproc; grep -m1 "model name" /proc/cpuinfo; grep -o -w -e avx512bw -e avx2 -e gfni /proc/cpuinfo | sort | uniq -c; cat /sys/fs/cgroup/cpu.max) > gpurun_out/cpuinfo.log 2>&1 ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 ;;
+    pmc)    run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu --steps 5
+            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 ;;
+  esac
+done
+echo "ALL DONE"
