@@ -37,8 +37,13 @@ WORKLOADS = {
                    desc="RS(10+2) encode+decode, 1 MiB objects, batch 1024/GPU, device-resident"),
     "enc": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(), ops=("encode",),
                 desc="RS(10+2) encode, 1 MiB objects, batch 1024/GPU, device-resident"),
-    "dec4": dict(k=10, p=4, nbytes=4 << 20, batch=512, lost=(0, 5), ops=("decode",),
-                 desc="RS(10+4) decode, 2 missing data shards {0,5}, 4 MiB objects, batch 512/GPU"),
+    # a healthy RS(10+4) Get receives exactly k = 10 bodies (proxy first-d
+    # rule): data {0,5} and parity {12,13} absent; ReconstructData rebuilds
+    # the 2 data shards from the 10 survivors
+    "dec4": dict(k=10, p=4, nbytes=4 << 20, batch=512, lost=(0, 5), absent=(12, 13),
+                 ops=("decode",), data_only=True,
+                 desc="RS(10+4) ReconstructData, data shards {0,5} missing (10 of 14 present), "
+                      "4 MiB objects, batch 512/GPU"),
 }
 METRICS = {
     "encdec": "RS(10+2) encode+decode GiB/s (device-resident), 1 MB objects, 1/2/4/8 GPU",
@@ -66,7 +71,7 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16):
     S = (w["nbytes"] + k - 1) // k
     ns, _, pitch = sample.shape
     lost = list(w["lost"])
-    surv = [i for i in range(n) if i not in lost][:k]
+    surv = [i for i in range(n) if i not in lost and i not in w.get("absent", ())][:k]
     base = sample.reshape(-1)
 
     def one_pass():
@@ -132,16 +137,142 @@ def pmc_traffic(kernel_key):
         return None
 
 
+def run_trace(args):
+    """BASELINE config 5: mixed 4 KiB-100 MiB objects (log-uniform, numpy
+    PCG64 seed 20200225, 512 objects, ~5 GiB), RS(10+2), one MI355X, host <->
+    device copies INCLUDED: objects live in pinned host memory in Split
+    layout; a step = encode_batch (H2D data rows -> kernel -> D2H parity) +
+    decode_batch with data shards {0,5} missing (H2D 10 survivors -> kernel ->
+    D2H 2 rows).  Prints one JSON line (this is a DESIGN.md measurement, not
+    the headline metric)."""
+    import torch
+
+    import infinicache_amd as ia
+
+    k, p = 10, 2
+    n = k + p
+    rng = np.random.Generator(np.random.PCG64(20200225))
+    nobj = args.trace_objects
+    sizes = np.exp(rng.uniform(np.log(4096), np.log(100 << 20), nobj)).astype(np.int64)
+    S = (sizes + k - 1) // k
+    offs = np.concatenate([[0], np.cumsum(n * S)])
+    total_obj = int(sizes.sum())
+    enc = ia.New(k, p)
+    host = ia.host_alloc(int(offs[-1]))
+    # random object bytes: one 256 MiB device random block, copied around
+    rnd = torch.randint(0, 256, (256 << 20,), dtype=torch.uint8, device="cuda").cpu().numpy()
+    objs = []
+    for o in range(nobj):
+        base = host[offs[o]:offs[o + 1]]
+        nb = int(sizes[o])
+        st = (o * 7919 * 4096) % (len(rnd) - (100 << 20) - 1)
+        base[:nb] = rnd[st:st + nb]
+        base[nb:] = 0
+        objs.append([base[i * S[o]:(i + 1) * S[o]] for i in range(n)])
+    lost = (0, 5)
+    present = [[i not in lost for i in range(n)]] * nobj
+    golden = [[objs[o][i].copy() for i in lost] for o in range(0, nobj, 37)]
+
+    def step():
+        enc.encode_batch(objs)
+        oks = enc.decode_batch(objs, present=present)
+        assert all(oks)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    el = time.perf_counter() - t0
+    for j, o in enumerate(range(0, nobj, 37)):
+        for g, i in zip(golden[j], lost):
+            assert np.array_equal(objs[o][i], g), "decode did not restore the data rows"
+    e2e = 2 * total_obj * args.steps / el / GiB
+
+    # the same trace device-resident (kernel + launch only, no PCIe)
+    pitches = [(int(x) + 255) // 256 * 256 for x in S]
+    doffs = np.concatenate([[0], np.cumsum([n * pp for pp in pitches])])
+    dev = torch.zeros(int(doffs[-1]), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    pres = [i not in lost for i in range(n)]
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def dstep():
+        for o in range(nobj):
+            b = dev.data_ptr() + int(doffs[o])
+            enc.encode_dev(b, int(S[o]), pitches[o], n * pitches[o], 1, stream)
+            enc.decode_dev(b, pres, int(S[o]), pitches[o], n * pitches[o], 1, bad, stream)
+
+    dstep()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        dstep()
+    torch.cuda.synchronize()
+    dev_el = time.perf_counter() - t1
+    dev_rate = 2 * total_obj * args.steps / dev_el / GiB
+
+    cpu = None
+    if not args.no_cpu:
+        import oracle
+        from oracle import rs_numpy as rn
+        m = enc.matrix()
+        surv = [i for i in range(n) if i not in lost][:k]
+        inv_rows = rn.invert(m[surv])[list(lost)]
+        threads = int(os.environ.get("BENCH_CPU_THREADS", "16"))
+        t2 = time.perf_counter()
+        done = 0
+        for o in range(nobj):
+            sh = objs[o]
+            oracle.code_fast(m[k:], sh[:k], nthreads=threads, max_goroutines=32)
+            oracle.code_fast(inv_rows, [sh[i] for i in surv], nthreads=threads, max_goroutines=32)
+            done += 2 * int(sizes[o])
+            if time.perf_counter() - t2 > args.cpu_seconds:
+                break
+        cel = time.perf_counter() - t2
+        cpu = {"value": round(done / cel / GiB, 3), "unit": "GiB/s", "cores": threads,
+               "kind": "port",
+               "sample": f"per-object codeSomeShardsP (maxGoroutines 32) encode+decode over "
+                         f"{o + 1} trace objects ({done / GiB:.2f} GiB), host memory, no PCIe"}
+    out = {
+        "metric": "RS(10+2) encode+decode GiB/s, mixed 4 KiB-100 MiB trace, host<->device copies included",
+        "value": round(e2e, 2),
+        "unit": "GiB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: log-uniform sizes (PCG64 seed 20200225), random bytes, pinned host memory",
+        "config": {"workload": "config 5 mixed trace, e2e (pinned H2D -> gf_apply -> D2H, 4 slots/streams)",
+                   "objects": nobj, "total_object_bytes": total_obj,
+                   "size_min": int(sizes.min()), "size_max": int(sizes.max()),
+                   "size_median": int(np.median(sizes))},
+        "device_resident_same_trace_GiBps": round(dev_rate, 2),
+        "kernel_fraction_of_e2e_time": round(dev_el / el, 4),
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace"])
+    ap.add_argument("--trace-objects", type=int, default=512)
     ap.add_argument("--batch", type=int, default=0, help="objects per GPU (default: workload's)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
+
+    if args.workload == "trace":
+        return run_trace(args)
 
     import torch
     import torch.distributed as dist
@@ -176,7 +307,7 @@ def main():
     buf = torch.randint(0, 256, (nobj, n, pitch), dtype=torch.uint8, device=dev, generator=g)
     buf[:, :, S:] = 0
     bad = torch.zeros(nobj, dtype=torch.int32, device=dev)
-    present = [i not in w["lost"] for i in range(n)]
+    present = [i not in w["lost"] and i not in w.get("absent", ()) for i in range(n)]
     if "encode" not in w["ops"]:  # decode-only workload: start from valid parity
         enc.encode_dev(buf, S, pitch, stride, nobj, stream)
 
@@ -188,7 +319,11 @@ def main():
         if evs is not None:
             evs[1].record(stream)
         if "decode" in w["ops"]:
-            enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, stream)
+            if w.get("data_only"):
+                enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=True,
+                                    stream=stream)
+            else:
+                enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, stream)
         if evs is not None:
             evs[2].record(stream)
 
@@ -264,7 +399,7 @@ def main():
         else:
             sample[:, list(w["lost"])] = 0  # CPU reconstructs the erased rows
         m = enc.matrix()
-        surv = [i for i in range(n) if i not in w["lost"]][:k]
+        surv = [i for i in range(n) if present[i]][:k]
         inv_rows = rn.invert(m[surv])[list(w["lost"])] if w["lost"] else None
         cpu = cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=args.cpu_seconds,
                            threads=int(os.environ.get("BENCH_CPU_THREADS", "16")))

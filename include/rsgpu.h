@@ -104,8 +104,8 @@ int rsgpu_reconstruct(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens
 
 /* Fused Client.decode (ecRedis.go:404-427: Reconstruct, then Verify) in ONE
  * device pass: reconstructs every missing shard in place and sets *ok to the
- * result the upstream Verify-after-Reconstruct would return.  Returns
- * without device work (ok = 1) when nothing is missing and verify passes. */
+ * result the upstream Verify-after-Reconstruct would return.  With every
+ * shard present it is Client.decode's first Verify (*ok = its result). */
 int rsgpu_decode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards, int *ok);
 
 /* Update (upstream Update): for each non-nil newdata[c] (new_lens[c] != 0):
@@ -143,6 +143,32 @@ int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, 
  * d_bad[o] = 1 when upstream's Verify-after-Reconstruct would fail for o. */
 int rsgpu_decode_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                      size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream);
+
+/* ---- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
+ * The path starts and ends in host memory (ecRedis.go:96 Set buffer,
+ * ecRedis.go:161-170 gathered Get buffers).  These calls stream a batch of
+ * objects through the GPU over a ring of device slots / HIP streams so the
+ * copies of one object overlap the kernel of another; they return when every
+ * output is in host memory.  Host buffers should be pinned
+ * (rsgpu_host_register / rsgpu_host_alloc) for the copies to run async. */
+
+/* objs[o]: the Split() backing array of object o — data+parity rows of
+ * shard_lens[o] bytes each, contiguous (pitch = shard length).  Parity rows
+ * are written in place (Encode, ecRedis.go:390). */
+int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard_lens, int nobj);
+
+/* shards[o*(data+parity) + i]: buffer of shard i of object o (every entry
+ * non-NULL: missing ones receive the reconstruction), present[same index] != 0
+ * marks shards that arrived.  Fused Client.decode per object (ecRedis.go:404-
+ * 427): missing shards written, ok[o] = Verify-after-Reconstruct result. */
+int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *present,
+                       const size_t *shard_lens, int nobj, int *ok);
+
+/* Pinned host memory helpers (hipHostRegister / hipHostMalloc). */
+int rsgpu_host_register(void *p, size_t len);
+int rsgpu_host_unregister(void *p);
+int rsgpu_host_alloc(size_t len, void **out);
+int rsgpu_host_free(void *p);
 
 #ifdef __cplusplus
 }

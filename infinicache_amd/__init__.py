@@ -4,11 +4,13 @@ InfiniCache client (drop-in for reedsolomon.Encoder under
 from .ec import (DummyEncoder, ErrInvalidInput, ErrInvShardNum, ErrMaxShardNum,  # noqa: F401
                  ErrNotImplemented, ErrReconstructRequired, ErrShardNoData, ErrShardSize,
                  ErrShortData, ErrSingular, ErrTooFewShards, HipError, InvalidArgument, New,
-                 NewEncoder, NoDevice, RSEncoder, RSError, device_count, device_ok)
+                 NewEncoder, NoDevice, RSEncoder, RSError, device_count, device_ok, host_alloc,
+                 host_register, host_unregister)
 
 __all__ = [
     "New", "NewEncoder", "RSEncoder", "DummyEncoder", "RSError", "device_count", "device_ok",
     "ErrInvShardNum", "ErrMaxShardNum", "ErrTooFewShards", "ErrShardNoData", "ErrShardSize",
     "ErrSingular", "ErrShortData", "ErrReconstructRequired", "ErrInvalidInput",
-    "ErrNotImplemented", "InvalidArgument", "NoDevice", "HipError",
+    "ErrNotImplemented", "InvalidArgument", "NoDevice", "HipError", "host_alloc",
+    "host_register", "host_unregister",
 ]

@@ -1,0 +1,260 @@
+// ctx.h — internal: the rsgpu_ctx behind the opaque handle of include/rsgpu.h
+// (coding matrix, inverse/plan caches, staging slots, batch pipeline).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+#include "gf256.h"
+#include "gf_apply.h"
+
+namespace rsgpu {
+
+
+// One staging slot for the host-memory API: pinned host image + device image
+// of an object laid out [row][pitch], a stream and a mismatch flag.
+struct Slot {
+    uint8_t *h = nullptr, *d = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+    uint32_t *d_bad = nullptr, *h_bad = nullptr;
+    ~Slot() {
+        if (stream) (void)hipStreamDestroy(stream);
+        if (h) (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        if (d_bad) (void)hipFree(d_bad);
+        if (h_bad) (void)hipHostFree(h_bad);
+    }
+};
+
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+inline bool debug_on() {
+    static const bool on = std::getenv("RSGPU_DEBUG") != nullptr;
+    return on;
+}
+
+inline int hip_fail(hipError_t e, const char *what) {
+    if (debug_on()) std::fprintf(stderr, "rsgpu: %s failed: %s\n", what, hipGetErrorString(e));
+    return RSGPU_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+// Batch pipeline (pipeline.cpp): a ring of device slots, one stream each, so
+// H2D of object o+1 overlaps the kernel / D2H of object o.
+struct PipeSlot {
+    uint8_t *d = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+    uint32_t *d_bad = nullptr;
+    ~PipeSlot() {
+        if (stream) (void)hipStreamDestroy(stream);
+        if (d) (void)hipFree(d);
+        if (d_bad) (void)hipFree(d_bad);
+    }
+};
+
+struct Pipeline {
+    std::mutex mu;  // one batch at a time per context
+    std::vector<std::unique_ptr<PipeSlot>> slots;
+    uint32_t *h_bad = nullptr;  // pinned, one flag per object of the batch
+    size_t h_bad_cap = 0;
+    ~Pipeline() {
+        if (h_bad) (void)hipHostFree(h_bad);
+    }
+};
+
+}  // namespace rsgpu
+
+using namespace rsgpu;
+
+struct rsgpu_ctx {
+    rsgpu::Pipeline pipe;  // batch host API (pipeline.cpp)
+    int k = 0, p = 0, n = 0;
+    unsigned kind = 0;
+    int device = 0;
+    std::vector<uint8_t> m;  // n x k coding matrix
+
+    std::mutex mu;  // guards everything below
+    std::map<std::string, std::vector<uint8_t>> inverses;  // survivors -> k x k inverse
+    std::map<std::string, std::shared_ptr<Plan>> plans;
+    std::vector<std::unique_ptr<Slot>> free_slots;
+    int dev_state = 0;  // 0 unknown, 1 ok, <0 error code
+
+    const uint8_t *row(int r) const { return &m[(size_t)r * k]; }
+
+    // ---- device bring-up (lazy; per call hipSetDevice for thread safety)
+    int use_device() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (dev_state == 0) dev_state = rsgpu_device_ok(device) ? 1 : RSGPU_ERR_NO_DEVICE;
+            if (dev_state < 0) return dev_state;
+        }
+        HIP_TRY(hipSetDevice(device));
+        return RSGPU_OK;
+    }
+
+    // ---- survivors' inverse (upstream inversionTree.GetInvertedMatrix /
+    // InsertInvertedMatrix, keyed here by the survivor list, which is a
+    // function of upstream's invalidIndices key)
+    int inverse(const std::vector<int> &surv, std::vector<uint8_t> &inv) {
+        std::string key(surv.begin(), surv.end());
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = inverses.find(key);
+            if (it != inverses.end()) { inv = it->second; return RSGPU_OK; }
+        }
+        std::vector<uint8_t> sub((size_t)k * k);
+        for (int i = 0; i < k; ++i) std::memcpy(&sub[(size_t)i * k], row(surv[i]), k);
+        inv.assign((size_t)k * k, 0);
+        if (!gf_invert(sub.data(), k, inv.data())) return RSGPU_ERR_SINGULAR;
+        std::lock_guard<std::mutex> g(mu);
+        inverses.emplace(key, inv);
+        return RSGPU_OK;
+    }
+
+    std::shared_ptr<Plan> cached(const std::string &key) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = plans.find(key);
+        return it == plans.end() ? nullptr : it->second;
+    }
+    std::shared_ptr<Plan> remember(const std::string &key, std::shared_ptr<Plan> p) {
+        p->build_tables();
+        std::lock_guard<std::mutex> g(mu);
+        return plans.emplace(key, std::move(p)).first->second;
+    }
+
+    // Encode: rows [k, n) <- M[k:] x rows [0, k)
+    std::shared_ptr<Plan> plan_encode() {
+        if (auto p = cached("E")) return p;
+        auto p = std::make_shared<Plan>();
+        p->K = k; p->R = this->p; p->nw = this->p;
+        for (int c = 0; c < k; ++c) p->in_rows.push_back(c);
+        for (int r = k; r < n; ++r) {
+            p->out_rows.push_back(r);
+            p->coef.insert(p->coef.end(), row(r), row(r) + k);
+        }
+        return remember("E", p);
+    }
+
+    // Verify: check rows M[j] x data XOR parity_j == 0 for j in [k, n)
+    std::shared_ptr<Plan> plan_verify() {
+        if (auto p = cached("V")) return p;
+        auto p = std::make_shared<Plan>();
+        p->K = n; p->R = this->p; p->nw = 0;
+        for (int c = 0; c < n; ++c) p->in_rows.push_back(c);
+        for (int j = k; j < n; ++j) {
+            p->out_rows.push_back(-1);
+            for (int c = 0; c < n; ++c) p->coef.push_back(c < k ? row(j)[c] : (uint8_t)(c == j));
+        }
+        return remember("V", p);
+    }
+
+    // Reconstruct (upstream reconstruct()): survivors = first k present rows.
+    // Missing data row i = inv[i] x survivors; missing parity row j =
+    // (M[j] x inv) x survivors — the same bytes as upstream's second
+    // codeSomeShards over the (reconstructed) data rows, in one pass.
+    // With check = true (fused Client.decode), every present row beyond
+    // the survivors becomes a check row (M[j] x inv) x survivors XOR row_j:
+    // exactly the comparisons upstream's Verify-after-Reconstruct can fail;
+    // the survivors' own comparisons are identities (M[V] x inv = I).
+    int plan_reconstruct(const uint8_t *present, bool data_only, bool check,
+                         std::shared_ptr<Plan> &out) {
+        std::string key = check ? "D" : (data_only ? "d" : "R");
+        for (int i = 0; i < n; ++i) key.push_back(present[i] ? '1' : '0');
+        if ((out = cached(key))) return RSGPU_OK;
+        std::vector<int> surv, extra, miss;
+        for (int i = 0; i < n; ++i) {
+            if (present[i]) (surv.size() < (size_t)k ? surv : extra).push_back(i);
+            else miss.push_back(i);
+        }
+        std::vector<uint8_t> inv;
+        int e = inverse(surv, inv);
+        if (e) return e;
+        const GF &g = gf();
+        auto p = std::make_shared<Plan>();
+        p->in_rows = surv;
+        if (check) p->in_rows.insert(p->in_rows.end(), extra.begin(), extra.end());
+        p->K = (int)p->in_rows.size();
+        // coefficient row over survivors for an arbitrary matrix row j
+        auto over_surv = [&](int j, std::vector<uint8_t> &cr) {
+            cr.assign(p->K, 0);
+            if (j < k) {
+                std::memcpy(cr.data(), &inv[(size_t)j * k], k);
+                return;
+            }
+            for (int c = 0; c < k; ++c) {
+                const uint8_t mj = row(j)[c];
+                if (!mj) continue;
+                for (int s = 0; s < k; ++s) cr[s] ^= g.mul(mj, inv[(size_t)c * k + s]);
+            }
+        };
+        std::vector<uint8_t> cr;
+        for (int i : miss) {
+            if (data_only && i >= k) continue;
+            over_surv(i, cr);
+            p->out_rows.push_back(i);
+            p->coef.insert(p->coef.end(), cr.begin(), cr.end());
+        }
+        p->nw = (int)p->out_rows.size();
+        if (check) {
+            for (size_t x = 0; x < extra.size(); ++x) {
+                const int j = extra[x];
+                if (j < k) continue;  // upstream Verify compares parity rows only
+                over_surv(j, cr);
+                cr[k + x] ^= 1;
+                p->out_rows.push_back(-1);
+                p->coef.insert(p->coef.end(), cr.begin(), cr.end());
+            }
+        }
+        p->R = (int)p->out_rows.size();
+        out = remember(key, p);
+        return RSGPU_OK;
+    }
+
+    // ---- staging slots
+    int get_slot(size_t bytes, std::unique_ptr<Slot> &s) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_slots.empty()) { s = std::move(free_slots.back()); free_slots.pop_back(); }
+        }
+        if (!s) {
+            s.reset(new Slot());
+            HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+            HIP_TRY(hipMalloc(&s->d_bad, 4));
+            HIP_TRY(hipHostMalloc(&s->h_bad, 4, hipHostMallocDefault));
+        }
+        if (s->cap < bytes) {
+            if (s->h) (void)hipHostFree(s->h);
+            if (s->d) (void)hipFree(s->d);
+            s->h = nullptr; s->d = nullptr; s->cap = 0;
+            const size_t cap = round_up(bytes, (size_t)1 << 20);
+            HIP_TRY(hipHostMalloc(&s->h, cap, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&s->d, cap));
+            s->cap = cap;
+        }
+        return RSGPU_OK;
+    }
+    void put_slot(std::unique_ptr<Slot> s) {
+        std::lock_guard<std::mutex> g(mu);
+        free_slots.push_back(std::move(s));
+    }
+};
+
+namespace rsgpu {
+// upstream checkShards(shards, nilok): size = first non-empty length
+int check_shards(const size_t *lens, int n, bool nilok, size_t *size);
+}  // namespace rsgpu

@@ -35,6 +35,7 @@ struct Plan {
     std::vector<int> out_rows;   // R row indices (checked rows: unused)
     std::vector<uint8_t> coef;   // R x K
     std::vector<uint32_t> tab;   // [R][K][4] kernel tables
+    int ki = 0;                  // trailing identity inputs (gf_apply_kernel)
     // device copies for the generic (K > 16) kernel; uploaded once, then
     // immutable (safe for concurrent launches)
     uint32_t *d_tab = nullptr;     // [K][R][4] (input-major)

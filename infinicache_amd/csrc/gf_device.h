@@ -41,6 +41,7 @@ struct ApplyArgs {
     uint32_t nw;     // rows [0, nw) stored, [nw, R) compared to zero
     uint32_t span;   // bytes addressable from an object base
     uint32_t clear;  // the plan has no check rows: this pass zeroes bad[obj]
+    uint32_t ki;     // trailing identity inputs (see gf_apply_kernel)
     uint32_t in_off[K];
     uint32_t out_off[R];
     uint32_t tab[K * R * 4];  // input-major [K][R][4]: one s_load_dwordx(4R) per input
@@ -50,6 +51,12 @@ struct ApplyArgs {
 // Lane t handles vectors blockIdx.x*BS*U + t + u*BS, so every wave-wide
 // load/store is 1 KiB contiguous.  LAUX/SAUX are the buffer-op cache-policy
 // bits (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
+// Trailing identity inputs: the last `ki` inputs (runtime, <= R) each enter
+// exactly one row with coefficient 1 — input K-ki+j feeds row R-ki+j — and no
+// other row.  That is Verify's parity columns (check row = M[j] x data XOR
+// parity_j) and the fused decode's extra shards; the host detects it
+// (Plan::ki).  Those inputs cost one XOR instead of four v_perm + two XOR per
+// row, and one uniform branch per input (no per-coefficient branches).
 template <int K, int R, int U, int BS, int LAUX, int SAUX>
 __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
     const uint32_t v0 = blockIdx.x * (BS * U) + threadIdx.x;
@@ -81,16 +88,22 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
             for (int d = 0; d < 4; ++d) acc[r][d] = 0;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
+            if (c >= K - R && c >= K - (int)a.ki) {
+                // identity input: row R-K+c (compile-time index) ^= input
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const uint32_t w = x[u][c][d];
-                const uint32_t i0 = w & 0x03030303u;
-                const uint32_t i1 = (w >> 2) & 0x03030303u;
-                const uint32_t i2 = (w >> 4) & 0x03030303u;
-                const uint32_t i3 = (w >> 6) & 0x03030303u;
+                for (int d = 0; d < 4; ++d) acc[(R - K + c) < 0 ? 0 : (R - K + c)][d] ^= x[u][c][d];
+            } else {
 #pragma unroll
-                for (int r = 0; r < R; ++r)
-                    acc[r][d] = gf_mac(acc[r][d], &a.tab[(c * R + r) * 4], i0, i1, i2, i3);
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t w = x[u][c][d];
+                    const uint32_t i0 = w & 0x03030303u;
+                    const uint32_t i1 = (w >> 2) & 0x03030303u;
+                    const uint32_t i2 = (w >> 4) & 0x03030303u;
+                    const uint32_t i3 = (w >> 6) & 0x03030303u;
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r][d] = gf_mac(acc[r][d], &a.tab[(c * R + r) * 4], i0, i1, i2, i3);
+                }
             }
             // keep the input-at-a-time order: without these fences the IR
             // passes and the scheduler hoist every input's index math and

@@ -26,15 +26,16 @@
 
 namespace rsgpu {
 
-// Tuned launch shape of the specialised pass (tools/kbench.hip sweep on
-// MI355X): 256 lanes x one 16-B vector per row;
-// non-temporal (nt) input loads — every input byte is read exactly once, so
-// keeping it out of the caches frees them for the output write stream
-// (59% -> 75% of HBM peak); stores with sc0|sc1 (+2.5 points).
+// Tuned launch shape of the specialised pass (tools/kbench.hip sweeps on
+// MI355X): 256 lanes x one 16-B vector per row; non-temporal
+// (nt) input loads — every input byte is read exactly once, so keeping it
+// out of the caches frees them for the output write stream (59% -> 75% of
+// HBM peak); sc1 (system-scope, write-through) stores (+3-7 points on the
+// write-heavy plans, measured interleaved against sc0|sc1, nt and default).
 constexpr int kBlock = 256;    // lanes per workgroup
 constexpr int kUnroll = 1;     // 16-B vectors per lane
 constexpr int kLoadAux = 2;    // buffer_load: nt
-constexpr int kStoreAux = 17;  // buffer_store: sc0 | sc1
+constexpr int kStoreAux = 16;  // buffer_store: sc1
 constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
 constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
@@ -51,6 +52,16 @@ void Plan::build_tables() {
     tab.assign((size_t)R * K * 4, 0);
     for (int r = 0; r < R; ++r)
         for (int c = 0; c < K; ++c) coef_tables(coef[(size_t)r * K + c], &tab[((size_t)r * K + c) * 4]);
+    // trailing identity inputs: input K-ki+j has coefficient 1 in row R-ki+j
+    // and 0 in every other row
+    ki = 0;
+    for (int j = 1; j <= std::min(K, R); ++j) {
+        const int c = K - j, row = R - j;
+        bool unit = true;
+        for (int r = 0; r < R && unit; ++r) unit = coef[(size_t)r * K + c] == (r == row ? 1 : 0);
+        if (!unit) break;
+        ki = j;
+    }
 }
 
 Plan::~Plan() {
@@ -131,6 +142,9 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
     a.nvec = (uint32_t)((L.shard_len + 15) / 16);
     a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
     a.nw = (uint32_t)s.nw;
+    // identity inputs feed the plan's last ki rows; usable only when this
+    // pass is the plan's last pass (it holds those rows at the same offsets)
+    a.ki = (s.r0 + R == p.R) ? (uint32_t)std::min(p.ki, R) : 0u;
     int maxrow = 0;
     for (int c = 0; c < K; ++c) {
         a.in_off[c] = (uint32_t)(p.in_rows[c] * L.pitch);

@@ -1,0 +1,186 @@
+// pipeline.cpp — batched host-memory API: the path "starts and ends in host
+// memory" (the proxy socket buffer on Set, the gathered shard buffers on Get,
+// /root/reference/client/ecRedis.go:96 and :161-173), so a batch of objects is
+// streamed through the GPU as H2D -> gf_apply -> D2H over a ring of device
+// slots, one HIP stream per slot: the copy of object o+1 overlaps the kernel
+// and the copy-back of object o, and H2D / D2H use the two DMA directions.
+//
+//   rsgpu_encode_batch : Split-layout objects (rows contiguous, pitch = S as
+//                        produced by Split, ecRedis.go:384) -> parity in place
+//   rsgpu_decode_batch : per-object shard tables as gathered by EcGet
+//                        (12 separate buffers, ecRedis.go:161-170) -> missing
+//                        shards written, Verify-after-Reconstruct result
+//
+// The H2D copy repacks each object's rows to a 256-B device pitch
+// (hipMemcpy2DAsync), so any S (e.g. 104,858 = 2 mod 16) runs the aligned
+// kernel.  Host buffers should be pinned (rsgpu_host_register / _alloc) for
+// the copies to run asynchronously.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "ctx.h"
+
+namespace {
+
+constexpr int kSlots = 4;
+
+int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
+    auto &P = ctx->pipe;
+    while ((int)P.slots.size() < kSlots) {
+        std::unique_ptr<PipeSlot> s(new PipeSlot());
+        HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        HIP_TRY(hipMalloc(&s->d_bad, 4));
+        P.slots.push_back(std::move(s));
+    }
+    for (auto &s : P.slots) {
+        if (s->cap >= bytes) continue;
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        if (s->d) (void)hipFree(s->d);
+        s->d = nullptr;
+        s->cap = 0;
+        const size_t cap = round_up(bytes, (size_t)1 << 20);
+        HIP_TRY(hipMalloc(&s->d, cap));
+        s->cap = cap;
+    }
+    return RSGPU_OK;
+}
+
+int ensure_flags(rsgpu_ctx *ctx, int nobj) {
+    auto &P = ctx->pipe;
+    if (P.h_bad_cap >= (size_t)nobj) return RSGPU_OK;
+    if (P.h_bad) (void)hipHostFree(P.h_bad);
+    P.h_bad = nullptr;
+    P.h_bad_cap = 0;
+    HIP_TRY(hipHostMalloc(&P.h_bad, (size_t)std::max(nobj, 1) * 4, hipHostMallocDefault));
+    P.h_bad_cap = (size_t)std::max(nobj, 1);
+    return RSGPU_OK;
+}
+
+int drain(rsgpu_ctx *ctx) {
+    hipError_t first = hipSuccess;
+    for (auto &s : ctx->pipe.slots) {
+        hipError_t e = hipStreamSynchronize(s->stream);
+        if (first == hipSuccess) first = e;
+    }
+    return first == hipSuccess ? RSGPU_OK : hip_fail(first, "pipeline drain");
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsgpu_host_register(void *p, size_t len) {
+    if (!p || !len) return RSGPU_ERR_INVALID_ARG;
+    if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
+    HIP_TRY(hipHostRegister(p, len, hipHostRegisterDefault));
+    return RSGPU_OK;
+}
+
+int rsgpu_host_unregister(void *p) {
+    if (!p) return RSGPU_ERR_INVALID_ARG;
+    HIP_TRY(hipHostUnregister(p));
+    return RSGPU_OK;
+}
+
+int rsgpu_host_alloc(size_t len, void **out) {
+    if (!out || !len) return RSGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
+    HIP_TRY(hipHostMalloc(out, len, hipHostMallocDefault));
+    return RSGPU_OK;
+}
+
+int rsgpu_host_free(void *p) {
+    if (!p) return RSGPU_OK;
+    HIP_TRY(hipHostFree(p));
+    return RSGPU_OK;
+}
+
+int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard_lens, int nobj) {
+    if (!ctx || (nobj > 0 && (!objs || !shard_lens)) || nobj < 0) return RSGPU_ERR_INVALID_ARG;
+    const int k = ctx->k, p = ctx->p, n = ctx->n;
+    size_t maxbytes = 0;
+    for (int o = 0; o < nobj; ++o) {
+        if (!objs[o]) return RSGPU_ERR_INVALID_ARG;
+        if (shard_lens[o] == 0) return RSGPU_ERR_SHARD_NO_DATA;
+        maxbytes = std::max(maxbytes, (size_t)n * round_up(shard_lens[o], 256));
+    }
+    if (nobj == 0) return RSGPU_OK;
+    int e = ctx->use_device();
+    if (e) return e;
+    auto plan = ctx->plan_encode();
+    std::lock_guard<std::mutex> g(ctx->pipe.mu);
+    if ((e = ensure_slots(ctx, maxbytes))) return e;
+    hipError_t he = hipSuccess;
+    for (int o = 0; o < nobj && he == hipSuccess; ++o) {
+        PipeSlot &s = *ctx->pipe.slots[o % kSlots];
+        const size_t S = shard_lens[o], P = round_up(S, 256);
+        he = hipMemcpy2DAsync(s.d, P, objs[o], S, S, k, hipMemcpyHostToDevice, s.stream);
+        if (he == hipSuccess) he = launch_plan(*plan, Layout{s.d, 0, P, S, 1}, nullptr, s.stream);
+        if (he == hipSuccess)
+            he = hipMemcpy2DAsync(objs[o] + (size_t)k * S, S, s.d + (size_t)k * P, P, S, p,
+                                  hipMemcpyDeviceToHost, s.stream);
+    }
+    e = drain(ctx);
+    if (he != hipSuccess) return hip_fail(he, "rsgpu_encode_batch");
+    return e;
+}
+
+int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *present,
+                       const size_t *shard_lens, int nobj, int *ok) {
+    if (!ctx || nobj < 0 || (nobj > 0 && (!shards || !present || !shard_lens || !ok)))
+        return RSGPU_ERR_INVALID_ARG;
+    const int k = ctx->k, n = ctx->n;
+    size_t maxbytes = 0;
+    std::vector<std::shared_ptr<Plan>> plans(nobj);
+    for (int o = 0; o < nobj; ++o) {
+        const uint8_t *pr = present + (size_t)o * n;
+        int np = 0;
+        for (int i = 0; i < n; ++i) np += pr[i] != 0;
+        if (shard_lens[o] == 0) return RSGPU_ERR_SHARD_NO_DATA;
+        if (np < k) return RSGPU_ERR_TOO_FEW_SHARDS;
+        for (int i = 0; i < n; ++i)
+            if (!shards[(size_t)o * n + i]) return RSGPU_ERR_INVALID_ARG;  // outputs need buffers
+        int e = np == n ? (plans[o] = ctx->plan_verify(), RSGPU_OK)
+                        : ctx->plan_reconstruct(pr, false, true, plans[o]);
+        if (e) return e;
+        maxbytes = std::max(maxbytes, (size_t)n * round_up(shard_lens[o], 256));
+    }
+    if (nobj == 0) return RSGPU_OK;
+    int e = ctx->use_device();
+    if (e) return e;
+    std::lock_guard<std::mutex> g(ctx->pipe.mu);
+    if ((e = ensure_slots(ctx, maxbytes))) return e;
+    if ((e = ensure_flags(ctx, nobj))) return e;
+    hipError_t he = hipSuccess;
+    for (int o = 0; o < nobj && he == hipSuccess; ++o) {
+        PipeSlot &s = *ctx->pipe.slots[o % kSlots];
+        Plan &plan = *plans[o];
+        uint8_t *const *row = shards + (size_t)o * n;
+        const size_t S = shard_lens[o], P = round_up(S, 256);
+        for (int c = 0; c < plan.K && he == hipSuccess; ++c)
+            he = hipMemcpyAsync(s.d + (size_t)plan.in_rows[c] * P, row[plan.in_rows[c]], S,
+                                hipMemcpyHostToDevice, s.stream);
+        const bool checks = plan.nw < plan.R;
+        if (he == hipSuccess && checks) he = hipMemsetAsync(s.d_bad, 0, 4, s.stream);
+        if (he == hipSuccess)
+            he = launch_plan(plan, Layout{s.d, 0, P, S, 1}, checks ? s.d_bad : nullptr, s.stream);
+        for (int r = 0; r < plan.nw && he == hipSuccess; ++r)
+            he = hipMemcpyAsync(row[plan.out_rows[r]], s.d + (size_t)plan.out_rows[r] * P, S,
+                                hipMemcpyDeviceToHost, s.stream);
+        if (he == hipSuccess) {
+            if (checks)
+                he = hipMemcpyAsync(ctx->pipe.h_bad + o, s.d_bad, 4, hipMemcpyDeviceToHost, s.stream);
+            else
+                ctx->pipe.h_bad[o] = 0;
+        }
+    }
+    e = drain(ctx);
+    if (he != hipSuccess) return hip_fail(he, "rsgpu_decode_batch");
+    if (e) return e;
+    for (int o = 0; o < nobj; ++o) ok[o] = ctx->pipe.h_bad[o] == 0;
+    return RSGPU_OK;
+}
+
+}  // extern "C"

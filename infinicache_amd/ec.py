@@ -317,6 +317,98 @@ class RSEncoder:
                                         nobj, _dptr(bad), _stream_handle(stream)))
 
 
+    # -- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
+    def encode_batch(self, objs: Sequence) -> None:
+        """Encode many objects, each given as its Split() result (or the
+        backing array of one): parity rows are written in place.  Host
+        buffers from host_alloc()/host_register() make the copies async."""
+        bases, lens, keep = [], [], []
+        for o in objs:
+            if isinstance(o, (list, tuple)):
+                if len(o) != self.Shards:
+                    raise ErrTooFewShards()
+                rows = [_as_u8(s, True) for s in o]
+                S = len(rows[0])
+                if not all(len(r) == S and r.ctypes.data == rows[0].ctypes.data + i * S
+                           for i, r in enumerate(rows)):
+                    raise InvalidArgument("shards are not one contiguous Split() array")
+                ptr = rows[0].ctypes.data
+                keep.append(rows)
+            else:
+                arr = _as_u8(o, True)
+                if len(arr) % self.Shards:
+                    raise InvalidArgument("backing array length is not a multiple of the shard count")
+                S = len(arr) // self.Shards
+                ptr = arr.ctypes.data
+                keep.append(arr)
+            bases.append(ptr)
+            lens.append(S)
+        n = len(bases)
+        ptrs = (_lib.u8p * n)(*[ctypes.cast(ctypes.c_void_p(b), _lib.u8p) for b in bases])
+        ln = (ctypes.c_size_t * n)(*lens)
+        _check(self._L.rsgpu_encode_batch(self._ctx, ptrs, ln, n))
+
+    def decode_batch(self, objs: Sequence[list], present=None) -> List[bool]:
+        """Fused Client.decode over many Gets: objs[o] is the list of k+p
+        shards of object o (None/empty = did not arrive); missing shards are
+        filled in place.  With ``present`` (nobj x (k+p) flags) every entry is
+        a buffer and the flags say which ones arrived (no allocation).
+        Returns the per-object Verify-after-Reconstruct."""
+        nobj = len(objs)
+        n = self.Shards
+        ptrs = (_lib.u8p * (nobj * n))()
+        pres = (ctypes.c_uint8 * (nobj * n))()
+        lens = (ctypes.c_size_t * nobj)()
+        keep = []
+        for o, shards in enumerate(objs):
+            if len(shards) != n:
+                raise ErrTooFewShards()
+            S = next((len(s) for s in shards if s is not None and len(s)), 0)
+            if S == 0:
+                raise ErrShardNoData()
+            lens[o] = S
+            for i, s in enumerate(shards):
+                if present is not None:
+                    pres[o * n + i] = 1 if present[o][i] else 0
+                    if len(s) != S:
+                        raise ErrShardSize()
+                elif s is None or len(s) == 0:
+                    s = np.zeros(S, dtype=np.uint8)
+                    shards[i] = s
+                else:
+                    pres[o * n + i] = 1
+                    if len(s) != S:
+                        raise ErrShardSize()
+                a = _as_u8(s, not pres[o * n + i])
+                keep.append(a)
+                ptrs[o * n + i] = a.ctypes.data_as(_lib.u8p)
+        ok = (ctypes.c_int * max(nobj, 1))()
+        _check(self._L.rsgpu_decode_batch(self._ctx, ptrs, pres, lens, nobj, ok))
+        return [bool(ok[o]) for o in range(nobj)]
+
+
+def host_alloc(nbytes: int) -> np.ndarray:
+    """Pinned (page-locked) host buffer as a uint8 numpy array; freed with the
+    array.  Use it for objects streamed through encode_batch/decode_batch."""
+    L = _lib.load()
+    p = ctypes.c_void_p()
+    _check(L.rsgpu_host_alloc(nbytes, ctypes.byref(p)))
+    buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    import weakref
+    weakref.finalize(buf, L.rsgpu_host_free, ctypes.c_void_p(p.value))
+    return arr
+
+
+def host_register(arr: np.ndarray) -> None:
+    """Pin an existing host buffer for async DMA (hipHostRegister)."""
+    _check(_lib.load().rsgpu_host_register(arr.ctypes.data, arr.nbytes))
+
+
+def host_unregister(arr: np.ndarray) -> None:
+    _check(_lib.load().rsgpu_host_unregister(arr.ctypes.data))
+
+
 def _join(k: int, dst, shards: Sequence, outSize: int) -> None:
     """upstream Join (identical logic in /root/reference/client/ec.go:83-121)."""
     if len(shards) < k:

@@ -377,3 +377,51 @@ def test_dev_many_objects_grid_y_split(gpu):
         want = oracle.apply(m[k:], [h[o, c] for c in range(k)])
         for r in range(p):
             assert np.array_equal(h[o, k + r], want[r]), o
+
+
+# --------------------------------------------- batched host-memory pipeline
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_encode_batch_mixed_sizes(gpu, pinned):
+    k, p = 10, 2
+    enc = ia.New(k, p)
+    sizes = [1, 9, 100, 4096, 104858, 3, 70001, 1 << 20, 555]
+    objs, wants = [], []
+    for i, nb in enumerate(sizes):
+        data = rn.splitmix64_bytes(SEED, 500 + i, nb)
+        sh = enc.Split(data)
+        if pinned:
+            buf = ia.host_alloc(len(sh) * len(sh[0]))
+            buf[:] = np.concatenate(sh)
+            S = len(sh[0])
+            sh = [buf[j * S:(j + 1) * S] for j in range(k + p)]
+        e, want = oracle.encode(k, p, [s.copy() for s in sh[:k]] + [bytes(len(sh[0]))] * p)
+        objs.append(sh)
+        wants.append(want)
+    enc.encode_batch(objs)
+    for sh, want in zip(objs, wants):
+        for r in range(k, k + p):
+            assert np.array_equal(sh[r], want[r])
+
+
+def test_decode_batch_mixed_patterns(gpu):
+    k, p = 10, 4
+    enc = ia.New(k, p)
+    cases = [((0, 5), 104858), ((1, 2), 999), ((), 5000), ((7,), 1), ((10, 11), 4097),
+             ((0, 1, 2, 3), 65536)]
+    objs, fulls = [], []
+    for i, (lost, S) in enumerate(cases):
+        full = _full(k, p, S, idx=600 + i)
+        fulls.append(full)
+        objs.append([None if j in lost else full[j].copy() for j in range(k + p)])
+    # corrupt an extra shard of case 1 (12 present: 2 extras are checked)
+    objs[1][12][0] ^= 1
+    e, want1 = oracle.reconstruct(k, p, [None if x is None else x.copy() for x in objs[1]])
+    ok = enc.decode_batch(objs)
+    assert ok == [True, False, True, True, True, True]
+    for i, (lost, S) in enumerate(cases):
+        for j in range(k + p):
+            if i == 1:
+                assert np.array_equal(objs[i][j], want1[j])
+            else:
+                assert np.array_equal(objs[i][j], fulls[i][j]), (i, j)

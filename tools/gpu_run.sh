@@ -25,8 +25,13 @@ for s in $STEPS; do
     bench_all)
             run bench_enc 300 python bench.py --workload enc --no-cpu
             run bench_dec4 300 python bench.py --workload dec4 --no-cpu ;;
-    kbench) run kbench 300 ./tools/kbench 30 ;;
-    kbench) run kbench 300 ./tools/kbench 30 ;;
+    trace)  run bench_trace 900 python bench.py --workload trace --steps 3 --warmup 1 ;;
+    kbench) for sh in ${KSHAPES:-enc10_2 dec10_2 enc10_4 rdata10_4 decx10_4 ver10_2 ver10_4}; do
+              run kbench_$sh 300 ./tools/kbench $sh 15
+            done ;;
+    kbench) for sh in ${KSHAPES:-enc10_2 dec10_2 enc10_4 rdata10_4 decx10_4 ver10_2 ver10_4}; do
+              run kbench_$sh 300 ./tools/kbench $sh 15
+            done ;;
     cpuinfo) (nproc; grep -m1 "model name" /proc/cpuinfo; grep -o -w -e avx512bw -e avx2 -e gfni /proc/cpuinfo | sort | uniq -c; cat /sys/fs/cgroup/cpu.max) > gpurun_out/cpuinfo.log 2>&1 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 ;;
     pmc)    run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu --steps 5

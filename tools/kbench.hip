@@ -1,14 +1,16 @@
 // kbench.hip — interleaved A/B timing of gf_apply_kernel launch variants on
-// the BASELINE shape (RS(10+2), 1 MiB objects, batch 1024, [obj][row][pitch]).
+// real codec plans (built by the library itself, so check-row plans run on
+// consistent data), layout [obj][row][pitch] in HBM.
 //
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../infinicache_amd/csrc kbench.hip -o kbench
-//   ./kbench [rounds] [k p nbytes nobj]
+//   make -C tools kbench          (links ../infinicache_amd/librsgpu.so)
+//   ./tools/kbench SHAPE [rounds]
+//   SHAPE: enc10_2 | enc10_4 | dec10_2 | rdata10_4 | decx10_4 | ver10_2 | ver10_4
 //
-// Every variant's parity is checked bit-exact against variant 0 (which the
-// product's tests pin to the oracle).  A "xor-only" variant (same streams, no
-// GF math) and a plain copy give the memory-system ceilings for this access
-// pattern.  Timing: one HIP-event pair per launch, variants interleaved
-// round-robin in one process (methodology rule 24); median and best reported.
+// Every variant's output rows are checked bit-exact against the library's own
+// launch (which the product tests pin to the oracle); check-row plans must
+// report no mismatch.  An xor-only kernel with the same streams gives the
+// memory-pattern ceiling.  Timing: one HIP-event pair per launch, variants
+// interleaved round-robin in one process (methodology rule 24).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -18,35 +20,19 @@
 #include <string>
 #include <vector>
 
-#include "gf256.h"
+#include "ctx.h"
 #include "gf_device.h"
-
-namespace rsgpu {
-const GF &gf() {
-    static const GF g;
-    return g;
-}
-}  // namespace rsgpu
 
 using namespace rsgpu;
 
-#define CK(x)                                                                       \
-    do {                                                                            \
-        hipError_t e_ = (x);                                                        \
-        if (e_ != hipSuccess) {                                                     \
+#define CK(x)                                                                                      \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
             std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
-            std::exit(1);                                                           \
-        }                                                                           \
+            std::exit(1);                                                                          \
+        }                                                                                          \
     } while (0)
-
-static void tables(uint8_t c, uint32_t out[4]) {
-    const GF &g = gf();
-    for (int grp = 0; grp < 4; ++grp) {
-        uint32_t w = 0;
-        for (int j = 0; j < 4; ++j) w |= (uint32_t)g.mul(c, (uint8_t)(j << (2 * grp))) << (8 * j);
-        out[grp] = w;
-    }
-}
 
 __global__ void fill(uint8_t *p, size_t n, uint64_t seed) {
     size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x);
@@ -59,7 +45,7 @@ __global__ void fill(uint8_t *p, size_t n, uint64_t seed) {
     }
 }
 
-// memory-pattern ceiling: identical loads/stores, XOR instead of GF multiply
+// memory-pattern ceiling: same loads/stores as the plan, XOR instead of GF math
 template <int K, int R>
 __global__ __launch_bounds__(256) void xor_only(const ApplyArgs<K, R> a) {
     const uint32_t v = blockIdx.x * 256 + threadIdx.x;
@@ -69,147 +55,191 @@ __global__ __launch_bounds__(256) void xor_only(const ApplyArgs<K, R> a) {
         __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
     u32x4 x[K];
 #pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.in_off[c], 0);
-    u32x4 acc[R];
+    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.in_off[c], 2);
+    u32x4 acc = x[0];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        acc[r] = x[0] ^ (u32x4){(uint32_t)r, 0, 0, 0};
-#pragma unroll
-        for (int c = 1; c < K; ++c) acc[r] ^= x[c];
-        __builtin_amdgcn_raw_buffer_store_b128(acc[r], rs, v * 16u, a.out_off[r], 0);
-    }
+    for (int c = 1; c < K; ++c) acc ^= x[c];
+    for (uint32_t r = 0; r < a.nw; ++r)
+        __builtin_amdgcn_raw_buffer_store_b128(acc, rs, v * 16u, a.out_off[r], 16);
+    if (a.nw == 0 && acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) a.bad[0] = 1;  // keep live
 }
 
-__global__ void copy16(const uint4 *__restrict__ s, uint4 *__restrict__ d, size_t n) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    for (; i < n; i += (size_t)gridDim.x * blockDim.x) d[i] = s[i];
+typedef void (*launch_fn)(const void *, dim3, hipStream_t);
+template <int K, int R, int U, int BS, int LA, int SA, bool NOKI = false>
+void launch_v(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    if (NOKI) a.ki = 0;  // every input through the dense GF path
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA>), grid, dim3(BS), 0, st, a);
+}
+template <int K, int R>
+void launch_x(const void *args, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((xor_only<K, R>), grid, dim3(256), 0, st, *(const ApplyArgs<K, R> *)args);
 }
 
 struct Variant {
     std::string name;
-    void (*launch)(const void *args, dim3 grid, hipStream_t);
+    launch_fn fn;
     int U, BS;
+    bool ceiling;
 };
 
-template <int K, int R, int U, int BS, int LA, int SA>
-void launch_v(const void *args, dim3 grid, hipStream_t st) {
-    const ApplyArgs<K, R> &a = *(const ApplyArgs<K, R> *)args;
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA>), grid, dim3(BS), 0, st, a);
-}
 template <int K, int R>
-void launch_xor(const void *args, dim3 grid, hipStream_t st) {
-    const ApplyArgs<K, R> &a = *(const ApplyArgs<K, R> *)args;
-    hipLaunchKernelGGL((xor_only<K, R>), grid, dim3(256), 0, st, a);
+std::vector<Variant> variants() {
+    return {
+        {"shipped(U1,B256,nt/sc1)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
+        {"no identity inputs", launch_v<K, R, 1, 256, 2, 16, true>, 1, 256, false},
+        {"nt/sc01", launch_v<K, R, 1, 256, 2, 17>, 1, 256, false},
+        {"default-policy", launch_v<K, R, 1, 256, 0, 0>, 1, 256, false},
+        {"nt/nt", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"B128 nt/sc1", launch_v<K, R, 1, 128, 2, 16>, 1, 128, false},
+        {"B512 nt/sc1", launch_v<K, R, 1, 512, 2, 16>, 1, 512, false},
+        {"U2 nt/sc1", launch_v<K, R, 2, 256, 2, 16>, 2, 256, false},
+        {"xor-only ceiling", launch_x<K, R>, 1, 256, true},
+    };
 }
 
-constexpr int K = 10, R = 2;
-
-int main(int argc, char **argv) {
-    const int rounds = argc > 1 ? std::atoi(argv[1]) : 30;
-    const size_t nbytes = 1 << 20;
-    const int nobj = 1024;
-    const size_t S = (nbytes + K - 1) / K;
-    const size_t pitch = (S + 255) / 256 * 256;
-    const int n = K + R;
-    const size_t stride = n * pitch;
-    const size_t total = stride * nobj;
-
-    // RS(10+2) parity rows (upstream buildMatrix; see oracle KATs)
-    const uint8_t rows[2][10] = {{0x81, 0x96, 0xaf, 0xb8, 0xd2, 0xc4, 0xfe, 0xe8, 0x03, 0x02},
-                                 {0x96, 0x81, 0xb8, 0xaf, 0xc4, 0xd2, 0xe8, 0xfe, 0x02, 0x03}};
-    ApplyArgs<K, R> a;
-    std::memset(&a, 0, sizeof(a));
-    a.obj_stride = stride;
-    a.nvec = (uint32_t)((S + 15) / 16);
-    a.tail = (uint32_t)(S - (a.nvec - 1) * 16);
-    a.nw = R;
-    a.span = (uint32_t)((n - 1) * pitch + a.nvec * 16);
-    for (int c = 0; c < K; ++c) a.in_off[c] = (uint32_t)(c * pitch);
-    for (int r = 0; r < R; ++r) a.out_off[r] = (uint32_t)((K + r) * pitch);
-    for (int c = 0; c < K; ++c)
-        for (int r = 0; r < R; ++r) tables(rows[r][c], &a.tab[(c * R + r) * 4]);
-
+template <int K, int R>
+int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
+    const int n = ctx->n;
+    const size_t pitch = (S + 255) / 256 * 256, stride = n * pitch, total = stride * nobj;
     uint8_t *d;
     CK(hipMalloc(&d, total));
-    uint8_t *dcopy;
-    CK(hipMalloc(&dcopy, total));
+    uint32_t *bad;
+    CK(hipMalloc(&bad, nobj * 4));
     hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, total, 12345ull);
     CK(hipDeviceSynchronize());
-    a.base = d;
+    // consistent parity for check-row plans
+    if (rsgpu_encode_dev(ctx, d, S, pitch, stride, nobj, nullptr)) return 1;
+    CK(hipDeviceSynchronize());
 
-    std::vector<Variant> vs = {
-        {"U1_B256", launch_v<K, R, 1, 256, 0, 0>, 1, 256},
-        {"ldnt_B256", launch_v<K, R, 1, 256, 2, 0>, 1, 256},
-        {"ldnt_B128", launch_v<K, R, 1, 128, 2, 0>, 1, 128},
-        {"ldnt_B512", launch_v<K, R, 1, 512, 2, 0>, 1, 512},
-        {"ldnt_U2_B256", launch_v<K, R, 2, 256, 2, 0>, 2, 256},
-        {"ldnt_U2_B128", launch_v<K, R, 2, 128, 2, 0>, 2, 128},
-        {"ldnt_stsc1", launch_v<K, R, 1, 256, 2, 16>, 1, 256},
-        {"ldnt_stsc01", launch_v<K, R, 1, 256, 2, 17>, 1, 256},
-        {"ldntsc1_B256", launch_v<K, R, 1, 256, 18, 0>, 1, 256},
-        {"ldntsc0_B256", launch_v<K, R, 1, 256, 3, 0>, 1, 256},
-        {"ldsc1_B256", launch_v<K, R, 1, 256, 16, 0>, 1, 256},
-        {"ldsc0_B256", launch_v<K, R, 1, 256, 1, 0>, 1, 256},
-        {"ldnt_stnt_B512", launch_v<K, R, 1, 512, 2, 2>, 1, 512},
-        {"xor_only", launch_xor<K, R>, 1, 256},
-    };
-    const int nv = (int)vs.size();
-    std::vector<uint8_t> ref(total), got(total);
+    ApplyArgs<K, R> a;
+    std::memset(&a, 0, sizeof(a));
+    a.base = d;
+    a.obj_stride = stride;
+    a.bad = bad;
+    a.nvec = (uint32_t)((S + 15) / 16);
+    a.tail = (uint32_t)(S - (a.nvec - 1) * 16);
+    a.nw = (uint32_t)plan.nw;
+    a.clear = plan.nw == plan.R;
+    a.ki = (uint32_t)plan.ki;
+    int maxrow = 0;
+    for (int c = 0; c < K; ++c) {
+        a.in_off[c] = (uint32_t)(plan.in_rows[c] * pitch);
+        maxrow = std::max(maxrow, plan.in_rows[c]);
+    }
+    for (int r = 0; r < R; ++r) {
+        const int row = plan.out_rows[r];
+        a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
+        maxrow = std::max(maxrow, row);
+        for (int c = 0; c < K; ++c)
+            for (int g = 0; g < 4; ++g) a.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
+    }
+    a.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
+
     hipStream_t st;
     CK(hipStreamCreate(&st));
-    // reference parity from variant 0
-    vs[0].launch(&a, dim3((a.nvec + 255) / 256, nobj), st);
+    std::vector<Variant> vs = variants<K, R>();
+    const int nv = (int)vs.size();
+    auto grid = [&](const Variant &v) {
+        return dim3((a.nvec + v.BS * v.U - 1) / (v.BS * v.U), nobj);
+    };
+    // reference output from the library's own pass
+    CK(hipMemset(bad, 0, nobj * 4));
+    CK(launch_plan(plan, Layout{d, stride, pitch, S, nobj}, bad, st));
     CK(hipStreamSynchronize(st));
+    std::vector<uint8_t> ref(total), got(total);
+    std::vector<uint32_t> hb(nobj);
     CK(hipMemcpy(ref.data(), d, total, hipMemcpyDeviceToHost));
-    std::vector<bool> exact(nv, true);
-    for (int v = 1; v < nv - 1; ++v) {
-        CK(hipMemset(d + 0, 0, 0));
-        // clobber parity rows, rerun, compare
-        for (int o = 0; o < nobj; o += 97) CK(hipMemset(d + o * stride + K * pitch, 0x5A, R * pitch));
-        const unsigned gx = (a.nvec + vs[v].BS * vs[v].U - 1) / (vs[v].BS * vs[v].U);
-        vs[v].launch(&a, dim3(gx, nobj), st);
+    CK(hipMemcpy(hb.data(), bad, nobj * 4, hipMemcpyDeviceToHost));
+    for (int o = 0; o < nobj; ++o)
+        if (hb[o]) { std::printf("library pass flagged object %d\n", o); return 1; }
+    std::vector<std::string> status(nv);
+    for (int v = 0; v < nv; ++v) {
+        if (vs[v].ceiling) { status[v] = "(pattern ceiling)"; continue; }
+        for (int r = 0; r < plan.nw; ++r)
+            for (int o = 0; o < nobj; o += 61)
+                CK(hipMemset(d + o * stride + plan.out_rows[r] * pitch, 0x5A, S));
+        CK(hipMemset(bad, 0xFF, nobj * 4));
+        vs[v].fn(&a, grid(vs[v]), st);
         CK(hipStreamSynchronize(st));
         CK(hipMemcpy(got.data(), d, total, hipMemcpyDeviceToHost));
-        for (int o = 0; o < nobj && exact[v]; ++o)
-            for (int r = 0; r < R; ++r)
-                if (std::memcmp(&got[o * stride + (K + r) * pitch], &ref[o * stride + (K + r) * pitch], S))
-                    exact[v] = false;
+        CK(hipMemcpy(hb.data(), bad, nobj * 4, hipMemcpyDeviceToHost));
+        bool ok = true;
+        for (int o = 0; o < nobj && ok; ++o) {
+            if (plan.nw < plan.R && hb[o] != 0xFFFFFFFFu) ok = false;  // no spurious flags
+            if (plan.nw == plan.R && hb[o] != 0) ok = false;          // cleared by the pass
+            for (int r = 0; r < plan.nw; ++r) {
+                const size_t off = o * stride + plan.out_rows[r] * pitch;
+                if (std::memcmp(&got[off], &ref[off], S)) ok = false;
+            }
+        }
+        status[v] = ok ? "bit-exact" : "MISMATCH";
     }
-    // timing, interleaved
-    std::vector<std::vector<float>> ms(nv + 1);
+    std::vector<std::vector<float>> ms(nv);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const size_t n16 = total / 16;
-    for (int it = 0; it < rounds + 3; ++it) {
-        for (int v = 0; v <= nv; ++v) {
+    for (int it = 0; it < rounds + 3; ++it)
+        for (int v = 0; v < nv; ++v) {
             CK(hipEventRecord(e0, st));
-            if (v < nv) {
-                const unsigned gx = (a.nvec + vs[v].BS * vs[v].U - 1) / (vs[v].BS * vs[v].U);
-                vs[v].launch(&a, dim3(gx, nobj), st);
-            } else {
-                hipLaunchKernelGGL(copy16, dim3(8192), dim3(256), 0, st, (const uint4 *)d, (uint4 *)dcopy, n16);
-            }
+            vs[v].fn(&a, grid(vs[v]), st);
             CK(hipEventRecord(e1, st));
             CK(hipEventSynchronize(e1));
             float t;
             CK(hipEventElapsedTime(&t, e0, e1));
             if (it >= 3) ms[v].push_back(t);
         }
-    }
-    const double alg = (double)nobj * (K + R) * S;
-    std::printf("shape: RS(%d+%d) S=%zu pitch=%zu nobj=%d  algorithmic bytes/launch=%.0f\n", K, R, S,
-                pitch, nobj, alg);
-    for (int v = 0; v <= nv; ++v) {
+    const double alg = (double)nobj * (plan.K + plan.nw) * S;
+    std::printf("shape %s: K=%d R=%d (nw=%d, ki=%d) S=%zu nobj=%d, algorithmic bytes/launch %.0f\n",
+                shape, K, R, plan.nw, plan.ki, S, nobj, alg);
+    for (int v = 0; v < nv; ++v) {
         std::vector<float> x = ms[v];
         std::sort(x.begin(), x.end());
-        const double med = x[x.size() / 2], best = x[0];
-        const double bytes = v < nv ? alg : 2.0 * total;
-        std::printf("%-16s med %8.1f us  best %8.1f us  %7.1f GB/s (med)  %5.1f%% of 8 TB/s  %s\n",
-                    v < nv ? vs[v].name.c_str() : "copy16(2x total)", med * 1e3, best * 1e3,
-                    bytes / (med * 1e-3) / 1e9, 100.0 * bytes / (med * 1e-3) / 8e12,
-                    v < nv ? (v == 0 ? "ref" : (v == nv - 1 ? "(pattern ceiling)" : (exact[v] ? "bit-exact" : "MISMATCH")))
-                           : "");
+        const double med = x[x.size() / 2];
+        std::printf("  %-26s med %8.1f us  best %8.1f us  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n",
+                    vs[v].name.c_str(), med * 1e3, x[0] * 1e3, alg / (med * 1e-3) / 1e9,
+                    100.0 * alg / (med * 1e-3) / 8e12, status[v].c_str());
     }
+    CK(hipFree(d));
+    CK(hipFree(bad));
     return 0;
+}
+
+int main(int argc, char **argv) {
+    const std::string shape = argc > 1 ? argv[1] : "enc10_2";
+    const int rounds = argc > 2 ? std::atoi(argv[2]) : 20;
+    const bool p4 = shape.find("10_4") != std::string::npos;
+    const int k = 10, p = p4 ? 4 : 2, n = k + p;
+    const size_t nbytes = p4 ? (4u << 20) : (1u << 20);
+    const int nobj = p4 ? 512 : 1024;
+    const size_t S = (nbytes + k - 1) / k;
+    rsgpu_ctx *ctx;
+    if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
+    if (ctx->use_device()) { std::printf("no device\n"); return 1; }
+    std::vector<uint8_t> present(n, 1);
+    std::shared_ptr<Plan> plan;
+    if (shape.rfind("enc", 0) == 0) {
+        plan = ctx->plan_encode();
+    } else if (shape.rfind("ver", 0) == 0) {
+        plan = ctx->plan_verify();
+    } else if (shape == "dec10_2") {  // healthy Get: data {0,5} missing, fused decode
+        present[0] = present[5] = 0;
+        ctx->plan_reconstruct(present.data(), false, true, plan);
+    } else if (shape == "rdata10_4") {  // config 3: 10 of 14 present, ReconstructData
+        present[0] = present[5] = present[12] = present[13] = 0;
+        ctx->plan_reconstruct(present.data(), true, false, plan);
+    } else if (shape == "decx10_4") {  // fused decode with 2 extra (checked) parity shards
+        present[0] = present[5] = 0;
+        ctx->plan_reconstruct(present.data(), false, true, plan);
+    } else {
+        std::printf("unknown shape %s\n", shape.c_str());
+        return 1;
+    }
+    const int K = plan->K, R = plan->R;
+#define SHAPE(k_, r_) \
+    if (K == k_ && R == r_) return run<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str());
+    SHAPE(10, 2) SHAPE(10, 4) SHAPE(12, 2) SHAPE(12, 4) SHAPE(14, 4)
+#undef SHAPE
+    std::printf("no instantiation for K=%d R=%d\n", K, R);
+    return 1;
 }
