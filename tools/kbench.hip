@@ -205,9 +205,85 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
     return 0;
 }
 
+// Pitch sweep: the shipped variant of one plan on layouts whose row pitch is
+// roundup(S, 256) + pad, interleaved in one process (HBM channel effects).
+template <int K, int R>
+int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
+    const int n = ctx->n;
+    const size_t pads[] = {0, 256, 512, 1024, 2048, 4096, 4096 + 256, 65536 + 256};
+    const int np = sizeof(pads) / sizeof(pads[0]);
+    std::vector<uint8_t *> bufs(np);
+    std::vector<ApplyArgs<K, R>> args(np);
+    uint32_t *bad;
+    CK(hipMalloc(&bad, nobj * 4));
+    for (int i = 0; i < np; ++i) {
+        const size_t pitch = (S + 255) / 256 * 256 + pads[i], stride = n * pitch;
+        CK(hipMalloc(&bufs[i], stride * nobj));
+        hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, bufs[i], stride * nobj, 777ull);
+        CK(hipDeviceSynchronize());
+        if (rsgpu_encode_dev(ctx, bufs[i], S, pitch, stride, nobj, nullptr)) return 1;
+        ApplyArgs<K, R> &a = args[i];
+        std::memset(&a, 0, sizeof(a));
+        a.base = bufs[i];
+        a.obj_stride = stride;
+        a.bad = bad;
+        a.nvec = (uint32_t)((S + 15) / 16);
+        a.tail = (uint32_t)(S - (a.nvec - 1) * 16);
+        a.nw = (uint32_t)plan.nw;
+        a.clear = plan.nw == plan.R;
+        a.ki = (uint32_t)plan.ki;
+        int maxrow = 0;
+        for (int c = 0; c < K; ++c) {
+            a.in_off[c] = (uint32_t)(plan.in_rows[c] * pitch);
+            maxrow = std::max(maxrow, plan.in_rows[c]);
+        }
+        for (int r = 0; r < R; ++r) {
+            const int row = plan.out_rows[r];
+            a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
+            maxrow = std::max(maxrow, row);
+            for (int c = 0; c < K; ++c)
+                for (int g = 0; g < 4; ++g) a.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
+        }
+        a.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
+    }
+    CK(hipDeviceSynchronize());
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<std::vector<float>> ms(np);
+    const dim3 grid((args[0].nvec + 255) / 256, nobj);
+    for (int it = 0; it < rounds + 3; ++it)
+        for (int i = 0; i < np; ++i) {
+            CK(hipEventRecord(e0, st));
+            launch_v<K, R, 1, 256, 2, 16>(&args[i], grid, st);
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            if (it >= 3) ms[i].push_back(t);
+        }
+    const double alg = (double)nobj * (plan.K + plan.nw) * S;
+    std::printf("pitch sweep %s: K=%d R=%d S=%zu nobj=%d\n", shape, K, R, S, nobj);
+    for (int i = 0; i < np; ++i) {
+        std::vector<float> x = ms[i];
+        std::sort(x.begin(), x.end());
+        const double med = x[x.size() / 2];
+        const size_t pitch = (S + 255) / 256 * 256 + pads[i];
+        std::printf("  pitch %8zu (+%5zu)  med %8.1f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n", pitch, pads[i],
+                    med * 1e3, alg / (med * 1e-3) / 1e9, 100.0 * alg / (med * 1e-3) / 8e12);
+    }
+    for (auto b : bufs) CK(hipFree(b));
+    CK(hipFree(bad));
+    return 0;
+}
+
 int main(int argc, char **argv) {
-    const std::string shape = argc > 1 ? argv[1] : "enc10_2";
+    std::string shape = argc > 1 ? argv[1] : "enc10_2";
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 20;
+    const bool sweep = shape.rfind("pitch:", 0) == 0;  // pitch:SHAPE
+    if (sweep) shape = shape.substr(6);
     const bool p4 = shape.find("10_4") != std::string::npos;
     const int k = 10, p = p4 ? 4 : 2, n = k + p;
     const size_t nbytes = p4 ? (4u << 20) : (1u << 20);
@@ -236,8 +312,10 @@ int main(int argc, char **argv) {
         return 1;
     }
     const int K = plan->K, R = plan->R;
-#define SHAPE(k_, r_) \
-    if (K == k_ && R == r_) return run<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str());
+#define SHAPE(k_, r_)                                                                       \
+    if (K == k_ && R == r_)                                                                 \
+        return sweep ? pitch_sweep<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str())      \
+                     : run<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str());
     SHAPE(10, 2) SHAPE(10, 4) SHAPE(12, 2) SHAPE(12, 4) SHAPE(14, 4)
 #undef SHAPE
     std::printf("no instantiation for K=%d R=%d\n", K, R);
