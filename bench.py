@@ -126,6 +126,65 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16):
     }
 
 
+class DistCtx:
+    """The only cross-rank traffic of the path: an all_reduce of one int as
+    the start/finish barrier (RCCL over xGMI on GPUs, gloo on CPU) and one
+    MAX-reduce of the elapsed time.  Objects never cross ranks."""
+
+    def __init__(self, world, rank, device):
+        self.world, self.rank, self.device = world, rank, device
+
+    def barrier(self):
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            t = torch.ones(1, dtype=torch.int32, device=self.device)
+            dist.all_reduce(t)
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: int) -> int:
+        if self.world == 1:
+            return x
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.int64, device=self.device)
+        dist.all_reduce(t)
+        return int(t.item())
+
+
+def shard_objects(nobj_total: int, rank: int, world: int):
+    """Contiguous object range of `rank` for strong scaling (objects are
+    independent units: object i's shards never leave its rank's GPU)."""
+    base, rem = divmod(nobj_total, world)
+    start = rank * base + min(rank, rem)
+    return start, base + (1 if rank < rem else 0)
+
+
+def timed_run(step, steps, warmup, sync, dctx: DistCtx):
+    """W untimed warmup steps; barrier + sync; K timed steps; sync + barrier +
+    sync; returns the MAX over ranks of the elapsed seconds."""
+    for _ in range(warmup):
+        step(None)
+    sync()
+    dctx.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    dctx.barrier()
+    sync()
+    return dctx.max(time.perf_counter() - t0)
+
+
 def pmc_traffic(kernel_key):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (separate
     --pmc passes; gfx950 FETCH_SIZE x2 correction, MI355X_MICROARCH.md §HBM)."""
@@ -267,6 +326,8 @@ def main():
     ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace"])
     ap.add_argument("--trace-objects", type=int, default=512)
     ap.add_argument("--batch", type=int, default=0, help="objects per GPU (default: workload's)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the workload's batch is the TOTAL, split over ranks")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -296,6 +357,8 @@ def main():
     k, p = w["k"], w["p"]
     n = k + p
     nobj = args.batch or w["batch"]
+    if args.strong:
+        nobj = shard_objects(nobj, rank, world)[1]
     S = (w["nbytes"] + k - 1) // k
     pitch = (S + 255) // 256 * 256
     stride = n * pitch
@@ -327,29 +390,11 @@ def main():
         if evs is not None:
             evs[2].record(stream)
 
-    def barrier():
-        if world > 1:
-            t = torch.ones(1, dtype=torch.int32, device=dev)
-            dist.all_reduce(t)  # RCCL over xGMI: the only collective
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-
+    dctx = DistCtx(world, rank, dev)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize(dev)
-    barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_run(lambda i: step(None if i is None else evs[i]), args.steps, args.warmup,
+                        lambda: torch.cuda.synchronize(dev), dctx)
+    objs_all = dctx.sum(nobj)
 
     if int(bad.sum()) != 0:
         raise SystemExit("decode reported a verify mismatch on synthetic data")
@@ -357,7 +402,7 @@ def main():
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     ops = len(w["ops"])
-    total_obj_bytes = world * nobj * w["nbytes"] * ops * args.steps
+    total_obj_bytes = objs_all * w["nbytes"] * ops * args.steps
     value = total_obj_bytes / elapsed / GiB
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -414,7 +459,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic: uniform random bytes (torch.randint on device, seeded per rank)",
