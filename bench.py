@@ -35,6 +35,12 @@ WORKLOADS = {
     # name: (k, p, object bytes, batch per GPU, erased rows for decode, ops)
     "encdec": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(0, 5), ops=("encode", "decode"),
                    desc="RS(10+2) encode+decode, 1 MiB objects, batch 1024/GPU, device-resident"),
+    # the same with a realistic Get batch: every object lost its own random
+    # pair of shards (proxy first-d rule), decoded in one mixed-pattern launch
+    "encdec_mixed": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(0, 5), ops=("encode", "decode"),
+                         mixed=True,
+                         desc="RS(10+2) encode+decode, 1 MiB objects, batch 1024/GPU, per-object "
+                              "random erasure pair (mixed-pattern decode)"),
     "enc": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(), ops=("encode",),
                 desc="RS(10+2) encode, 1 MiB objects, batch 1024/GPU, device-resident"),
     # a healthy RS(10+4) Get receives exactly k = 10 bodies (proxy first-d
@@ -47,6 +53,7 @@ WORKLOADS = {
 }
 METRICS = {
     "encdec": "RS(10+2) encode+decode GiB/s (device-resident), 1 MB objects, 1/2/4/8 GPU",
+    "encdec_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 1 MB objects",
     "enc": "RS(10+2) encode GiB/s (device-resident), 1 MB objects",
     "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
 }
@@ -373,6 +380,11 @@ def main():
     present = [i not in w["lost"] and i not in w.get("absent", ()) for i in range(n)]
     if "encode" not in w["ops"]:  # decode-only workload: start from valid parity
         enc.encode_dev(buf, S, pitch, stride, nobj, stream)
+    if w.get("mixed"):  # per-object random erasure pair (seeded)
+        prs = np.random.default_rng(20200225 + rank)
+        pres_m = np.ones((nobj, n), dtype=np.uint8)
+        for o in range(nobj):
+            pres_m[o, prs.choice(n, p, replace=False)] = 0
 
     def step(evs=None):
         if evs is not None:
@@ -382,7 +394,9 @@ def main():
         if evs is not None:
             evs[1].record(stream)
         if "decode" in w["ops"]:
-            if w.get("data_only"):
+            if w.get("mixed"):
+                enc.decode_dev_multi(buf, pres_m, S, pitch, stride, nobj, bad, stream)
+            elif w.get("data_only"):
                 enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=True,
                                     stream=stream)
             else:

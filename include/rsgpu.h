@@ -144,6 +144,18 @@ int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, 
 int rsgpu_decode_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                      size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream);
 
+/* Mixed erasure patterns (a batch of Gets, each with its own first-d
+ * subset): present[o*(data+parity) + i] != 0 marks row i of object o present.
+ * One launch per (K, R) class; each workgroup fetches its object's pass
+ * (cached per pattern) through scalar loads.  Same per-object semantics as
+ * rsgpu_reconstruct_dev / rsgpu_decode_dev (objects with every shard present
+ * are skipped by reconstruct and verified by decode). */
+int rsgpu_reconstruct_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
+                                size_t shard_len, size_t pitch, size_t obj_stride, int nobj,
+                                int data_only, void *stream);
+int rsgpu_decode_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                           size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream);
+
 /* ---- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
  * The path starts and ends in host memory (ecRedis.go:96 Set buffer,
  * ecRedis.go:161-170 gathered Get buffers).  These calls stream a batch of

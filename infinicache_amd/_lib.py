@@ -19,7 +19,8 @@ EXPORTS = (
     "rsgpu_create", "rsgpu_destroy", "rsgpu_data_shards", "rsgpu_parity_shards", "rsgpu_matrix",
     "rsgpu_strerror", "rsgpu_device_count", "rsgpu_device_ok", "rsgpu_encode", "rsgpu_verify",
     "rsgpu_reconstruct", "rsgpu_decode", "rsgpu_update", "rsgpu_encode_dev", "rsgpu_verify_dev",
-    "rsgpu_reconstruct_dev", "rsgpu_decode_dev", "rsgpu_encode_batch", "rsgpu_decode_batch",
+    "rsgpu_reconstruct_dev", "rsgpu_decode_dev", "rsgpu_reconstruct_dev_multi",
+    "rsgpu_decode_dev_multi", "rsgpu_encode_batch", "rsgpu_decode_batch",
     "rsgpu_host_register", "rsgpu_host_unregister", "rsgpu_host_alloc", "rsgpu_host_free",
 )
 
@@ -77,6 +78,8 @@ def load():
     L.rsgpu_verify_dev.argtypes = [vp, vp, sz, sz, sz, ci, vp, vp]
     L.rsgpu_reconstruct_dev.argtypes = [vp, vp, u8p, sz, sz, sz, ci, ci, vp]
     L.rsgpu_decode_dev.argtypes = [vp, vp, u8p, sz, sz, sz, ci, vp, vp]
+    L.rsgpu_reconstruct_dev_multi.argtypes = [vp, vp, u8p, sz, sz, sz, ci, ci, vp]
+    L.rsgpu_decode_dev_multi.argtypes = [vp, vp, u8p, sz, sz, sz, ci, vp, vp]
     L.rsgpu_encode_batch.argtypes = [vp, u8pp, szp, ci]
     L.rsgpu_decode_batch.argtypes = [vp, u8pp, u8p, szp, ci, intp]
     L.rsgpu_host_register.argtypes = [vp, sz]

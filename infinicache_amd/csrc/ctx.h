@@ -83,6 +83,7 @@ using namespace rsgpu;
 
 struct rsgpu_ctx {
     rsgpu::Pipeline pipe;  // batch host API (pipeline.cpp)
+    rsgpu::MultiWorkspace multi_ws;  // mixed-pattern device launches
     int k = 0, p = 0, n = 0;
     unsigned kind = 0;
     int device = 0;

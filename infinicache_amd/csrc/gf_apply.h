@@ -54,6 +54,29 @@ struct Layout {
     int nobj;
 };
 
+// Device workspace for mixed-pattern launches (pass images + object lists),
+// reused across calls once the previous call's kernels finished with it.
+struct MultiWorkspace {
+    static constexpr int kRing = 4;  // images in flight before a host wait
+    struct Slot {
+        void *d = nullptr, *h = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+    };
+    std::mutex mu;
+    Slot slot[kRing];
+    unsigned next = 0;
+    ~MultiWorkspace();
+};
+
+// Object o of the layout is coded with plans[plan_of[o]] (a batch of Gets
+// with mixed erasure patterns): one launch per (K, R) class of sub-passes,
+// each workgroup fetching its object's pass by scalar loads.  d_bad follows
+// launch_plan's contract per object.
+hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vector<int> &plan_of,
+                              const Layout &L, uint32_t *d_bad, hipStream_t stream,
+                              MultiWorkspace &ws);
+
 // Launches the plan over all objects on `stream`.  d_bad (nobj u32) must be
 // zeroed by the caller when the plan has check rows.  Returns hipSuccess or
 // the first HIP error.

@@ -18,6 +18,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
 #include <mutex>
 
 #include "gf_apply.h"
@@ -36,6 +40,7 @@ constexpr int kBlock = 256;    // lanes per workgroup
 constexpr int kUnroll = 1;     // 16-B vectors per lane
 constexpr int kLoadAux = 2;    // buffer_load: nt
 constexpr int kStoreAux = 16;  // buffer_store: sc1
+constexpr int kMultiChunks = 1; // chunks per workgroup in the mixed-pattern kernel (kbench: 1 best)
 constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
 constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
@@ -135,42 +140,126 @@ struct Sub {  // one pass over <= kMaxR output rows of a plan
 };
 
 template <int K, int R>
+void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool have_bad, Pass<K, R> &a) {
+    a.nw = (uint32_t)s.nw;
+    // identity inputs feed the plan's last ki rows; usable only when this
+    // pass is the plan's last pass (it holds those rows at the same offsets)
+    a.ki = (s.r0 + R == p.R) ? (uint32_t)std::min(p.ki, R) : 0u;
+    a.clear = (have_bad && p.nw == p.R) ? 1u : 0u;
+    int maxrow = 0;
+    for (int c = 0; c < K; ++c) {
+        a.in_off[c] = (uint32_t)(p.in_rows[c] * pitch);
+        maxrow = std::max(maxrow, p.in_rows[c]);
+    }
+    for (int r = 0; r < R; ++r) {
+        const int row = p.out_rows[s.r0 + r];
+        a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
+        maxrow = std::max(maxrow, row);
+        for (int c = 0; c < K; ++c)
+            for (int g = 0; g < 4; ++g)
+                a.tab[(c * R + r) * 4 + g] = p.tab[((size_t)(s.r0 + r) * K + c) * 4 + g];
+    }
+    a.span = (uint32_t)((size_t)maxrow * pitch + (size_t)nvec * 16);
+}
+
+template <int K, int R>
 hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
                         hipStream_t st) {
     ApplyArgs<K, R> a;
     a.obj_stride = L.obj_stride;
     a.nvec = (uint32_t)((L.shard_len + 15) / 16);
     a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
-    a.nw = (uint32_t)s.nw;
-    // identity inputs feed the plan's last ki rows; usable only when this
-    // pass is the plan's last pass (it holds those rows at the same offsets)
-    a.ki = (s.r0 + R == p.R) ? (uint32_t)std::min(p.ki, R) : 0u;
-    int maxrow = 0;
-    for (int c = 0; c < K; ++c) {
-        a.in_off[c] = (uint32_t)(p.in_rows[c] * L.pitch);
-        maxrow = std::max(maxrow, p.in_rows[c]);
-    }
-    for (int r = 0; r < R; ++r) {
-        const int row = p.out_rows[s.r0 + r];
-        a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * L.pitch);
-        maxrow = std::max(maxrow, row);
-        for (int c = 0; c < K; ++c)
-            for (int g = 0; g < 4; ++g)
-                a.tab[(c * R + r) * 4 + g] = p.tab[((size_t)(s.r0 + r) * K + c) * 4 + g];
-    }
-    a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * 16);
+    fill_pass<K, R>(p, s, L.pitch, a.nvec, d_bad != nullptr, a.p);
     const unsigned gx = (a.nvec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
     for (int o0 = 0; o0 < L.nobj; o0 += kMaxGridY) {
         const int no = std::min(kMaxGridY, L.nobj - o0);
         a.base = L.base + (size_t)o0 * L.obj_stride;
         a.bad = d_bad ? d_bad + o0 : nullptr;
-        a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
         hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(gx, no),
                            dim3(kBlock), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// ---- mixed-pattern launch: one (K, R) class of (plan, sub-pass) entries
+
+struct Entry {  // one sub-pass of one plan and the objects that use it
+    const Plan *plan;
+    Sub sub;
+    std::vector<uint32_t> objs;
+};
+
+// Appends this class's device image — passes[], then objs[], obj_pass[] —
+// to `img` (16-B aligned pieces) and returns the launch closure.
+template <int K, int R>
+std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
+    const std::vector<const Entry *> &es, const Layout &L, uint32_t *d_bad, std::vector<uint8_t> &img) {
+    const uint32_t nvec = (uint32_t)((L.shard_len + 15) / 16);
+    auto align = [&]() { img.resize((img.size() + 15) & ~(size_t)15); };
+    align();
+    const size_t pass_off = img.size();
+    img.resize(pass_off + es.size() * sizeof(Pass<K, R>));
+    size_t nobj = 0;
+    for (size_t i = 0; i < es.size(); ++i) {
+        Pass<K, R> pp;
+        fill_pass<K, R>(*es[i]->plan, es[i]->sub, L.pitch, nvec, d_bad != nullptr, pp);
+        std::memcpy(&img[pass_off + i * sizeof(Pass<K, R>)], &pp, sizeof(pp));
+        nobj += es[i]->objs.size();
+    }
+    align();
+    const size_t objs_off = img.size();
+    img.resize(objs_off + nobj * 8);
+    uint32_t *objs = (uint32_t *)&img[objs_off], *pidx = objs + nobj;
+    size_t j = 0;
+    for (size_t i = 0; i < es.size(); ++i)
+        for (uint32_t o : es[i]->objs) {
+            objs[j] = o;
+            pidx[j] = (uint32_t)i;
+            ++j;
+        }
+    return [=](const uint8_t *dimg, hipStream_t st) -> hipError_t {
+        MultiArgs<K, R> m;
+        m.base = L.base;
+        m.obj_stride = L.obj_stride;
+        m.bad = d_bad;
+        m.nvec = nvec;
+        m.tail = (uint32_t)(L.shard_len - (size_t)(nvec - 1) * 16);
+        m.passes = (const Pass<K, R> *)(dimg + pass_off);
+        const unsigned per = kBlock * kUnroll * kMultiChunks;
+        const unsigned gx = (nvec + per - 1) / per;
+        for (size_t o0 = 0; o0 < nobj; o0 += kMaxGridY) {
+            const int no = (int)std::min((size_t)kMaxGridY, nobj - o0);
+            m.objs = (const uint32_t *)(dimg + objs_off) + o0;
+            m.obj_pass = (const uint32_t *)(dimg + objs_off) + nobj + o0;
+            hipLaunchKernelGGL((gf_apply_multi<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kMultiChunks>),
+                               dim3(gx, no), dim3(kBlock), 0, st, m);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
+}
+
+typedef std::function<hipError_t(const uint8_t *, hipStream_t)> (*stage_fn)(
+    const std::vector<const Entry *> &, const Layout &, uint32_t *, std::vector<uint8_t> &);
+
+template <int K>
+stage_fn pick_stage_r(int R) {
+    return R == 1 ? &stage_class<K, 1> : R == 2 ? &stage_class<K, 2> : R == 3 ? &stage_class<K, 3>
+                                                                                : &stage_class<K, 4>;
+}
+
+stage_fn pick_stage(int K, int R) {
+    switch (K) {
+#define RSGPU_K(k) case k: return pick_stage_r<k>(R);
+        RSGPU_K(1) RSGPU_K(2) RSGPU_K(3) RSGPU_K(4) RSGPU_K(5) RSGPU_K(6) RSGPU_K(7) RSGPU_K(8)
+        RSGPU_K(9) RSGPU_K(10) RSGPU_K(11) RSGPU_K(12) RSGPU_K(13) RSGPU_K(14) RSGPU_K(15)
+        RSGPU_K(16)
+#undef RSGPU_K
+        default: return nullptr;
+    }
 }
 
 template <int R>
@@ -274,6 +363,76 @@ hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+MultiWorkspace::~MultiWorkspace() {
+    for (auto &s : slot) {
+        if (s.done) (void)hipEventDestroy(s.done);
+        if (s.d) (void)hipFree(s.d);
+        if (s.h) (void)hipHostFree(s.h);
+    }
+}
+
+hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vector<int> &plan_of,
+                              const Layout &L, uint32_t *d_bad, hipStream_t st, MultiWorkspace &ws) {
+    // entries grouped into (K, R) classes; K > 16 plans run object by object
+    std::vector<std::vector<Entry>> per_plan(plans.size());
+    std::vector<std::vector<uint32_t>> objs_of(plans.size());
+    for (size_t o = 0; o < plan_of.size(); ++o)
+        if (plan_of[o] >= 0) objs_of[plan_of[o]].push_back((uint32_t)o);  // -1: skip object
+    std::map<std::pair<int, int>, std::vector<const Entry *>> classes;
+    std::vector<std::unique_ptr<Entry>> store;
+    for (size_t i = 0; i < plans.size(); ++i) {
+        Plan &p = *plans[i];
+        if (objs_of[i].empty() || p.R <= 0) continue;
+        if (p.K > kMaxK) {
+            for (uint32_t o : objs_of[i]) {
+                Layout one{L.base + (size_t)o * L.obj_stride, L.obj_stride, L.pitch, L.shard_len, 1};
+                hipError_t e = launch_plan(p, one, d_bad ? d_bad + o : nullptr, st);
+                if (e != hipSuccess) return e;
+            }
+            continue;
+        }
+        for (int r0 = 0; r0 < p.R; r0 += kMaxR) {
+            Sub s{r0, std::min(kMaxR, p.R - r0), 0};
+            s.nw = std::max(0, std::min(s.R, p.nw - r0));
+            store.emplace_back(new Entry{&p, s, objs_of[i]});
+            classes[{p.K, s.R}].push_back(store.back().get());
+        }
+    }
+    if (classes.empty()) return hipSuccess;
+    std::vector<uint8_t> img;
+    std::vector<std::pair<size_t, std::function<hipError_t(const uint8_t *, hipStream_t)>>> launches;
+    for (auto &kv : classes)
+        launches.emplace_back(0, pick_stage(kv.first.first, kv.first.second)(kv.second, L, d_bad, img));
+    std::lock_guard<std::mutex> g(ws.mu);
+    MultiWorkspace::Slot &w = ws.slot[ws.next++ % MultiWorkspace::kRing];
+    hipError_t e = hipSuccess;
+    if (w.done) {  // the kernels that read this image kRing calls ago must be done
+        e = hipEventSynchronize(w.done);
+        if (e != hipSuccess) return e;
+    } else {
+        e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    if (w.cap < img.size()) {
+        if (w.d) (void)hipFree(w.d);
+        if (w.h) (void)hipHostFree(w.h);
+        w.d = nullptr;
+        w.h = nullptr;
+        w.cap = 0;
+        const size_t cap = std::max<size_t>(img.size() * 2, 1 << 16);
+        e = hipMalloc(&w.d, cap);
+        if (e == hipSuccess) e = hipHostMalloc(&w.h, cap, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        w.cap = cap;
+    }
+    std::memcpy(w.h, img.data(), img.size());
+    e = hipMemcpyAsync(w.d, w.h, img.size(), hipMemcpyHostToDevice, st);
+    for (auto &l : launches)
+        if (e == hipSuccess) e = l.second((const uint8_t *)w.d, st);
+    if (e == hipSuccess) e = hipEventRecord(w.done, st);
+    return e;
 }
 
 }  // namespace rsgpu

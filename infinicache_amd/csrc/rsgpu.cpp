@@ -430,6 +430,66 @@ static int recon_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_
     return RSGPU_OK;
 }
 
+// Mixed erasure patterns: present is nobj x (data+parity).  Objects are
+// grouped by pattern (one cached plan each) and coded by one launch per
+// (K, R) class (launch_plans_multi).
+static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                           size_t pitch, size_t obj_stride, int nobj, bool data_only, bool check,
+                           uint32_t *d_bad, void *stream) {
+    if (!ctx || (nobj > 0 && !present)) return RSGPU_ERR_INVALID_ARG;
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    if (e) return e;
+    const int n = ctx->n;
+    std::map<std::string, int> idx;
+    std::vector<std::shared_ptr<Plan>> owned;
+    std::vector<Plan *> plans;
+    std::vector<int> plan_of(nobj, -1);
+    bool any_checks = false;
+    for (int o = 0; o < nobj; ++o) {
+        const uint8_t *pr = present + (size_t)o * n;
+        std::string key(n, '0');
+        int np = 0;
+        for (int i = 0; i < n; ++i) {
+            key[i] = pr[i] ? '1' : '0';
+            np += pr[i] != 0;
+        }
+        if (np < ctx->k) return RSGPU_ERR_TOO_FEW_SHARDS;
+        if (np == n && !check) continue;  // nothing to reconstruct
+        auto it = idx.find(key);
+        if (it == idx.end()) {
+            std::shared_ptr<Plan> p;
+            if (np == n) p = ctx->plan_verify();
+            else if ((e = ctx->plan_reconstruct(pr, data_only, check, p))) return e;
+            any_checks |= p->nw < p->R;
+            it = idx.emplace(key, (int)plans.size()).first;
+            owned.push_back(p);
+            plans.push_back(p.get());
+        }
+        plan_of[o] = it->second;
+    }
+    if ((e = ctx->use_device())) return e;
+    if (check && any_checks)
+        HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
+    Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
+    HIP_TRY(launch_plans_multi(plans, plan_of, L, check ? d_bad : nullptr, (hipStream_t)stream,
+                               ctx->multi_ws));
+    return RSGPU_OK;
+}
+
+int rsgpu_reconstruct_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
+                                size_t shard_len, size_t pitch, size_t obj_stride, int nobj,
+                                int data_only, void *stream) {
+    return recon_dev_multi(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, data_only != 0,
+                           false, nullptr, stream);
+}
+
+int rsgpu_decode_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                           size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream) {
+    if (!d_bad) return RSGPU_ERR_INVALID_ARG;
+    return recon_dev_multi(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, false, true, d_bad,
+                           stream);
+}
+
 int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                           size_t pitch, size_t obj_stride, int nobj, int data_only, void *stream) {
     return recon_dev(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, data_only != 0, false,

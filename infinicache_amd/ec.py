@@ -317,6 +317,23 @@ class RSEncoder:
                                         nobj, _dptr(bad), _stream_handle(stream)))
 
 
+    def _present_matrix(self, present, nobj):
+        pm = np.ascontiguousarray(np.asarray(present, dtype=np.uint8).reshape(nobj, self.Shards))
+        return pm, pm.ctypes.data_as(_lib.u8p)
+
+    def reconstruct_dev_multi(self, base, present, shard_len, pitch, obj_stride, nobj,
+                              data_only=False, stream=None):
+        """Per-object erasure patterns: present is (nobj, k+p) flags."""
+        pm, pp = self._present_matrix(present, nobj)
+        _check(self._L.rsgpu_reconstruct_dev_multi(self._ctx, _dptr(base), pp, shard_len, pitch,
+                                                   obj_stride, nobj, int(data_only),
+                                                   _stream_handle(stream)))
+
+    def decode_dev_multi(self, base, present, shard_len, pitch, obj_stride, nobj, bad, stream=None):
+        pm, pp = self._present_matrix(present, nobj)
+        _check(self._L.rsgpu_decode_dev_multi(self._ctx, _dptr(base), pp, shard_len, pitch,
+                                              obj_stride, nobj, _dptr(bad), _stream_handle(stream)))
+
     # -- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
     def encode_batch(self, objs: Sequence) -> None:
         """Encode many objects, each given as its Split() result (or the

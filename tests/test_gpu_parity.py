@@ -425,3 +425,66 @@ def test_decode_batch_mixed_patterns(gpu):
                 assert np.array_equal(objs[i][j], want1[j])
             else:
                 assert np.array_equal(objs[i][j], fulls[i][j]), (i, j)
+
+
+# ------------------------------------------------ mixed erasure patterns
+
+@pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 50001, 300), (10, 4, 7777, 120), (20, 4, 3000, 40)])
+def test_dev_decode_multi_random_patterns(gpu, k, p, S, nobj):
+    """A batch of Gets, each object with its own erasure pattern (0..p lost;
+    fewer lost than p leaves extra shards that are really checked)."""
+    n = k + p
+    pitch = (S + 255) // 256 * 256
+    stride = n * pitch
+    rng = np.random.default_rng(k * 1000 + p)
+    b = _dev_batch(nobj, n, S, pitch, seed=S + nobj)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    golden = b.clone()
+    present = np.ones((nobj, n), dtype=np.uint8)
+    corrupt = set()
+    for o in range(nobj):
+        nl = int(rng.integers(0, p + 1))
+        lost = rng.choice(n, nl, replace=False)
+        present[o, lost] = 0
+        b[o, torch.as_tensor(lost, dtype=torch.long)] = 0xA5
+        if nl < p and o % 7 == 0:  # an extra present shard exists: corrupt the last present row
+            last = int(np.nonzero(present[o])[0][-1])
+            if last >= k:  # upstream Verify checks parity rows only
+                b[o, last, 3] ^= 1
+                corrupt.add(o)
+    bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    enc.decode_dev_multi(b, present, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    flags = bad.cpu().numpy()
+    for o in range(nobj):
+        assert flags[o] == (1 if o in corrupt else 0), (o, present[o])
+        if o not in corrupt:
+            assert torch.equal(b[o, :, :S], golden[o, :, :S]), (o, present[o])
+
+
+def test_dev_reconstruct_multi_data_only(gpu):
+    k, p, S, nobj = 10, 4, 9000, 64
+    n = k + p
+    pitch = 9216
+    stride = n * pitch
+    b = _dev_batch(nobj, n, S, pitch, seed=11)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    golden = b.clone()
+    present = np.ones((nobj, n), dtype=np.uint8)
+    pats = list(itertools.combinations(range(n), 4))
+    for o in range(nobj):
+        lost = pats[(o * 37) % len(pats)]
+        present[o, list(lost)] = 0
+        for i in lost:
+            b[o, i] = 0
+    enc.reconstruct_dev_multi(b, present, S, pitch, stride, nobj, data_only=True, stream=s)
+    torch.cuda.synchronize()
+    for o in range(nobj):
+        assert torch.equal(b[o, :k, :S], golden[o, :k, :S]), o
+        for i in range(k, n):  # missing parity untouched (data_only)
+            if not present[o, i]:
+                assert not b[o, i].any()

@@ -52,28 +52,37 @@ __global__ __launch_bounds__(256) void xor_only(const ApplyArgs<K, R> a) {
     if (v >= a.nvec) return;
     const uint8_t *ob = a.base + (uint64_t)blockIdx.y * a.obj_stride;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.p.span, 0x00020000);
     u32x4 x[K];
 #pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.in_off[c], 2);
+    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.p.in_off[c], 2);
     u32x4 acc = x[0];
 #pragma unroll
     for (int c = 1; c < K; ++c) acc ^= x[c];
-    for (uint32_t r = 0; r < a.nw; ++r)
-        __builtin_amdgcn_raw_buffer_store_b128(acc, rs, v * 16u, a.out_off[r], 16);
-    if (a.nw == 0 && acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) a.bad[0] = 1;  // keep live
+    for (uint32_t r = 0; r < a.p.nw; ++r)
+        __builtin_amdgcn_raw_buffer_store_b128(acc, rs, v * 16u, a.p.out_off[r], 16);
+    if (a.p.nw == 0 && acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) a.bad[0] = 1;  // keep live
 }
 
 typedef void (*launch_fn)(const void *, dim3, hipStream_t);
 template <int K, int R, int U, int BS, int LA, int SA, bool NOKI = false>
 void launch_v(const void *args, dim3 grid, hipStream_t st) {
     ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
-    if (NOKI) a.ki = 0;  // every input through the dense GF path
+    if (NOKI) a.p.ki = 0;  // every input through the dense GF path
     hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA>), grid, dim3(BS), 0, st, a);
 }
 template <int K, int R>
 void launch_x(const void *args, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((xor_only<K, R>), grid, dim3(256), 0, st, *(const ApplyArgs<K, R> *)args);
+}
+
+// multi-pass variant: the same plan fetched per workgroup from device memory
+static const void *g_multi_args = nullptr;
+template <int K, int R, int CH>
+void launch_m(const void *, dim3 grid, hipStream_t st) {
+    grid.x = (grid.x + CH - 1) / CH;
+    hipLaunchKernelGGL((gf_apply_multi<K, R, 1, 256, 2, 16, CH>), grid, dim3(256), 0, st,
+                       *(const MultiArgs<K, R> *)g_multi_args);
 }
 
 struct Variant {
@@ -94,6 +103,10 @@ std::vector<Variant> variants() {
         {"B128 nt/sc1", launch_v<K, R, 1, 128, 2, 16>, 1, 128, false},
         {"B512 nt/sc1", launch_v<K, R, 1, 512, 2, 16>, 1, 512, false},
         {"U2 nt/sc1", launch_v<K, R, 2, 256, 2, 16>, 2, 256, false},
+        {"multi CH1", launch_m<K, R, 1>, 1, 256, false},
+        {"multi CH2", launch_m<K, R, 2>, 1, 256, false},
+        {"multi CH4", launch_m<K, R, 4>, 1, 256, false},
+        {"multi CH8", launch_m<K, R, 8>, 1, 256, false},
         {"xor-only ceiling", launch_x<K, R>, 1, 256, true},
     };
 }
@@ -119,22 +132,44 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
     a.bad = bad;
     a.nvec = (uint32_t)((S + 15) / 16);
     a.tail = (uint32_t)(S - (a.nvec - 1) * 16);
-    a.nw = (uint32_t)plan.nw;
-    a.clear = plan.nw == plan.R;
-    a.ki = (uint32_t)plan.ki;
+    a.p.nw = (uint32_t)plan.nw;
+    a.p.clear = plan.nw == plan.R;
+    a.p.ki = (uint32_t)plan.ki;
     int maxrow = 0;
     for (int c = 0; c < K; ++c) {
-        a.in_off[c] = (uint32_t)(plan.in_rows[c] * pitch);
+        a.p.in_off[c] = (uint32_t)(plan.in_rows[c] * pitch);
         maxrow = std::max(maxrow, plan.in_rows[c]);
     }
     for (int r = 0; r < R; ++r) {
         const int row = plan.out_rows[r];
-        a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
+        a.p.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
         maxrow = std::max(maxrow, row);
         for (int c = 0; c < K; ++c)
-            for (int g = 0; g < 4; ++g) a.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
+            for (int g = 0; g < 4; ++g) a.p.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
     }
-    a.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
+    a.p.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
+
+    // device pass image for the multi variant: one pass, identity object list
+    Pass<K, R> *d_pass;
+    uint32_t *d_objs;
+    CK(hipMalloc(&d_pass, sizeof(Pass<K, R>)));
+    CK(hipMalloc(&d_objs, nobj * 8));
+    CK(hipMemcpy(d_pass, &a.p, sizeof(Pass<K, R>), hipMemcpyHostToDevice));
+    {
+        std::vector<uint32_t> h(nobj * 2, 0);
+        for (int o = 0; o < nobj; ++o) h[o] = o;
+        CK(hipMemcpy(d_objs, h.data(), nobj * 8, hipMemcpyHostToDevice));
+    }
+    MultiArgs<K, R> ma;
+    ma.base = d;
+    ma.obj_stride = stride;
+    ma.bad = bad;
+    ma.nvec = a.nvec;
+    ma.tail = a.tail;
+    ma.passes = d_pass;
+    ma.objs = d_objs;
+    ma.obj_pass = d_objs + nobj;
+    g_multi_args = &ma;
 
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -229,22 +264,22 @@ int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, cons
         a.bad = bad;
         a.nvec = (uint32_t)((S + 15) / 16);
         a.tail = (uint32_t)(S - (a.nvec - 1) * 16);
-        a.nw = (uint32_t)plan.nw;
-        a.clear = plan.nw == plan.R;
-        a.ki = (uint32_t)plan.ki;
+        a.p.nw = (uint32_t)plan.nw;
+        a.p.clear = plan.nw == plan.R;
+        a.p.ki = (uint32_t)plan.ki;
         int maxrow = 0;
         for (int c = 0; c < K; ++c) {
-            a.in_off[c] = (uint32_t)(plan.in_rows[c] * pitch);
+            a.p.in_off[c] = (uint32_t)(plan.in_rows[c] * pitch);
             maxrow = std::max(maxrow, plan.in_rows[c]);
         }
         for (int r = 0; r < R; ++r) {
             const int row = plan.out_rows[r];
-            a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
+            a.p.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
             maxrow = std::max(maxrow, row);
             for (int c = 0; c < K; ++c)
-                for (int g = 0; g < 4; ++g) a.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
+                for (int g = 0; g < 4; ++g) a.p.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
         }
-        a.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
+        a.p.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
     }
     CK(hipDeviceSynchronize());
     hipStream_t st;
