@@ -11,10 +11,13 @@
 //                        (12 separate buffers, ecRedis.go:161-170) -> missing
 //                        shards written, Verify-after-Reconstruct result
 //
-// The H2D copy repacks each object's rows to a 256-B device pitch
-// (hipMemcpy2DAsync), so any S (e.g. 104,858 = 2 mod 16) runs the aligned
-// kernel.  Host buffers should be pinned (rsgpu_host_register / _alloc) for
-// the copies to run asynchronously.
+// PCIe copies are always 1D (tools/pcie_bench.hip on MI355X: a pinned 1D
+// H2D runs at 53-57 GB/s, a 2D host<->device copy with 105-KB rows at
+// 8.7 GB/s).  An object whose S is not a multiple of 16 (e.g. 104,858) is
+// therefore copied packed (pitch S) into a device staging area and repacked
+// on the device (D2D 2D copy, ~770 GB/s) to the 256-B pitch the kernel
+// needs; the parity rows go back the same way.  Host buffers should be
+// pinned (rsgpu_host_register / _alloc) for the copies to run async.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -104,7 +107,9 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
     for (int o = 0; o < nobj; ++o) {
         if (!objs[o]) return RSGPU_ERR_INVALID_ARG;
         if (shard_lens[o] == 0) return RSGPU_ERR_SHARD_NO_DATA;
-        maxbytes = std::max(maxbytes, (size_t)n * round_up(shard_lens[o], 256));
+        // aligned image + packed staging image
+        maxbytes = std::max(maxbytes, round_up((size_t)n * round_up(shard_lens[o], 256), 256) +
+                                          (size_t)n * shard_lens[o]);
     }
     if (nobj == 0) return RSGPU_OK;
     int e = ctx->use_device();
@@ -115,12 +120,20 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
     hipError_t he = hipSuccess;
     for (int o = 0; o < nobj && he == hipSuccess; ++o) {
         PipeSlot &s = *ctx->pipe.slots[o % kSlots];
-        const size_t S = shard_lens[o], P = round_up(S, 256);
-        he = hipMemcpy2DAsync(s.d, P, objs[o], S, S, k, hipMemcpyHostToDevice, s.stream);
+        const size_t S = shard_lens[o];
+        const bool packed = S % 16 == 0;  // rows already aligned: no repack
+        const size_t P = packed ? S : round_up(S, 256);
+        uint8_t *stage = packed ? s.d : s.d + round_up((size_t)n * P, 256);
+        he = hipMemcpyAsync(stage, objs[o], (size_t)k * S, hipMemcpyHostToDevice, s.stream);
+        if (he == hipSuccess && !packed)
+            he = hipMemcpy2DAsync(s.d, P, stage, S, S, k, hipMemcpyDeviceToDevice, s.stream);
         if (he == hipSuccess) he = launch_plan(*plan, Layout{s.d, 0, P, S, 1}, nullptr, s.stream);
+        if (he == hipSuccess && !packed)
+            he = hipMemcpy2DAsync(stage + (size_t)k * S, S, s.d + (size_t)k * P, P, S, p,
+                                  hipMemcpyDeviceToDevice, s.stream);
         if (he == hipSuccess)
-            he = hipMemcpy2DAsync(objs[o] + (size_t)k * S, S, s.d + (size_t)k * P, P, S, p,
-                                  hipMemcpyDeviceToHost, s.stream);
+            he = hipMemcpyAsync(objs[o] + (size_t)k * S, stage + (size_t)k * S, (size_t)p * S,
+                                hipMemcpyDeviceToHost, s.stream);
     }
     e = drain(ctx);
     if (he != hipSuccess) return hip_fail(he, "rsgpu_encode_batch");

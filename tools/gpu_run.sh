@@ -26,6 +26,7 @@ for s in $STEPS; do
             run bench_enc 300 python bench.py --workload enc --no-cpu
             run bench_dec4 300 python bench.py --workload dec4 --no-cpu
             run bench_mixed 300 python bench.py --workload encdec_mixed --no-cpu ;;
+    pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
     torchrun1) run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --no-cpu ;;
     trace)  run bench_trace 900 python bench.py --workload trace --steps 3 --warmup 1 ;;
