@@ -325,12 +325,88 @@ def run_trace(args):
     print(json.dumps(out), flush=True)
 
 
+def run_latency(args):
+    """The per-object path the Go shim takes (one EcSet / EcGet at a time,
+    host buffers in and out): Client.encode = Encode + Verify
+    (ecRedis.go:382-402) and Client.decode = Reconstruct + Verify of 2 lost
+    data shards, fused (ecRedis.go:404-427), on 1 MiB RS(10+2) objects.
+    Reports per-op latency percentiles beside the CPU port's per-object
+    codeSomeShardsP latency.  A DESIGN.md measurement, not the headline."""
+    import infinicache_amd as ia
+    import oracle
+    from oracle import rs_numpy as rn
+    k, p, nb = 10, 2, 1 << 20
+    enc = ia.New(k, p)
+    rng = np.random.default_rng(7)
+    nobj = 64
+    objs = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(nobj)]
+    res = {}
+    for pinned in (False, True):
+        lat_e, lat_d = [], []
+        for it in range(args.steps + args.warmup):
+            o = objs[it % nobj]
+            if pinned:
+                buf = ia.host_alloc((k + p) * ((nb + k - 1) // k))
+                S = len(buf) // (k + p)
+                buf[:nb] = o
+                buf[nb:] = 0
+                sh = [buf[i * S:(i + 1) * S] for i in range(k + p)]
+            else:
+                sh = enc.Split(o)
+            t0 = time.perf_counter()
+            enc.Encode(sh)
+            ok = enc.Verify(sh)
+            t1 = time.perf_counter()
+            assert ok
+            got = [None if i in (0, 5) else sh[i] for i in range(k + p)]
+            t2 = time.perf_counter()
+            ok = enc.DecodeVerify(got)
+            t3 = time.perf_counter()
+            assert ok and np.array_equal(got[0], sh[0])
+            if it >= args.warmup:
+                lat_e.append(t1 - t0)
+                lat_d.append(t3 - t2)
+        key = "pinned" if pinned else "pageable"
+        res[key] = {
+            "encode_verify_us_p50": round(float(np.percentile(lat_e, 50)) * 1e6, 1),
+            "encode_verify_us_p99": round(float(np.percentile(lat_e, 99)) * 1e6, 1),
+            "decode_us_p50": round(float(np.percentile(lat_d, 50)) * 1e6, 1),
+            "decode_us_p99": round(float(np.percentile(lat_d, 99)) * 1e6, 1),
+        }
+    # CPU port, same ops per object (codeSomeShardsP, 16 threads)
+    m = enc.matrix()
+    inv = rn.invert(m[[1, 2, 3, 4, 6, 7, 8, 9, 10, 11]])[[0, 5]]
+    threads = int(os.environ.get("BENCH_CPU_THREADS", "16"))
+    ce, cd = [], []
+    for it in range(args.steps + args.warmup):
+        sh = rn.split(objs[it % nobj].tobytes(), k, p)
+        t0 = time.perf_counter()
+        par = oracle.code_fast(m[k:], sh[:k], nthreads=threads, max_goroutines=32)
+        chk = oracle.code_fast(m[k:], sh[:k], nthreads=threads, max_goroutines=32)  # Verify
+        t1 = time.perf_counter()
+        surv = [sh[i] for i in (1, 2, 3, 4, 6, 7, 8, 9)] + par
+        oracle.code_fast(inv, surv, nthreads=threads, max_goroutines=32)
+        t2 = time.perf_counter()
+        if it >= args.warmup:
+            ce.append(t1 - t0)
+            cd.append(t2 - t1)
+    out = {
+        "metric": "RS(10+2) per-object host-API latency (Client.encode / Client.decode), 1 MiB objects",
+        "gpu": res,
+        "cpu_port_16_threads": {
+            "encode_verify_us_p50": round(float(np.percentile(ce, 50)) * 1e6, 1),
+            "decode_us_p50": round(float(np.percentile(cd, 50)) * 1e6, 1)},
+        "ops": args.steps,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace"])
+    ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace", "latency"])
     ap.add_argument("--trace-objects", type=int, default=512)
     ap.add_argument("--batch", type=int, default=0, help="objects per GPU (default: workload's)")
     ap.add_argument("--strong", action="store_true",
@@ -341,6 +417,8 @@ def main():
 
     if args.workload == "trace":
         return run_trace(args)
+    if args.workload == "latency":
+        return run_latency(args)
 
     import torch
     import torch.distributed as dist

@@ -29,6 +29,7 @@ for s in $STEPS; do
     pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
     torchrun1) run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --no-cpu ;;
+    latency) run bench_latency 600 python bench.py --workload latency --steps 200 --warmup 10 ;;
     trace)  run bench_trace 900 python bench.py --workload trace --steps 3 --warmup 1 ;;
     kbench) for sh in ${KSHAPES:-enc10_2 dec10_2 enc10_4 rdata10_4 decx10_4 ver10_2 ver10_4}; do
               run kbench_$sh 300 ./tools/kbench $sh 15
