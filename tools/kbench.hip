@@ -64,6 +64,65 @@ __global__ __launch_bounds__(256) void xor_only(const ApplyArgs<K, R> a) {
     if (a.p.nw == 0 && acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) a.bad[0] = 1;  // keep live
 }
 
+// Ablation: the north star's "LDS-staged log/exp tables" formulation.  The
+// 256-entry log table and the 510-entry exp table of GF(2^8)/0x11D are staged
+// in LDS once per workgroup; each byte of each input is multiplied by each
+// coefficient as exp[log[x] + log[c]] (x == 0 -> 0), i.e. one LDS byte
+// lookup for log[x] per input byte (shared by all rows) and one for exp per
+// (byte, row), then the bytes are re-packed into dwords.  Same loads/stores
+// and launch shape as the shipped kernel.
+__constant__ uint8_t c_logexp[256 + 512];
+template <int K, int R>
+__global__ __launch_bounds__(256) void lds_logexp(const ApplyArgs<K, R> a, const uint8_t *logc) {
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_exp[512];
+    for (int i = threadIdx.x; i < 256; i += 256) s_log[i] = c_logexp[i];
+    for (int i = threadIdx.x; i < 512; i += 256) s_exp[i] = c_logexp[256 + i];
+    __syncthreads();
+    const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= a.nvec) return;
+    const uint8_t *ob = a.base + (uint64_t)blockIdx.y * a.obj_stride;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.p.span, 0x00020000);
+    uint32_t acc[R][4] = {};
+    for (int c = 0; c < K; ++c) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.p.in_off[c], 2);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t byte = (x[d] >> (8 * b)) & 0xffu;
+                const uint32_t lx = s_log[byte];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t lc = logc[c * R + r];  // 255 encodes coefficient 0
+                    const uint32_t prod = (byte == 0 || lc == 255u) ? 0u : s_exp[lx + lc];
+                    acc[r][d] ^= prod << (8 * b);
+                }
+            }
+        }
+    }
+    bool mismatch = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if ((uint32_t)r < a.p.nw) {
+            u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+            __builtin_amdgcn_raw_buffer_store_b128(o, rs, v * 16u, a.p.out_off[r], 16);
+        } else {
+            const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+        }
+    }
+    if (mismatch) atomicOr(a.bad + blockIdx.y, 1u);
+    if (a.p.clear && v == 0) a.bad[blockIdx.y] = 0u;
+}
+static const uint8_t *g_logc = nullptr;
+template <int K, int R>
+void launch_lds(const void *args, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((lds_logexp<K, R>), grid, dim3(256), 0, st, *(const ApplyArgs<K, R> *)args, g_logc);
+}
+
 typedef void (*launch_fn)(const void *, dim3, hipStream_t);
 template <int K, int R, int U, int BS, int LA, int SA, bool NOKI = false>
 void launch_v(const void *args, dim3 grid, hipStream_t st) {
@@ -103,6 +162,7 @@ std::vector<Variant> variants() {
         {"B128 nt/sc1", launch_v<K, R, 1, 128, 2, 16>, 1, 128, false},
         {"B512 nt/sc1", launch_v<K, R, 1, 512, 2, 16>, 1, 512, false},
         {"U2 nt/sc1", launch_v<K, R, 2, 256, 2, 16>, 2, 256, false},
+        {"LDS log/exp tables (ablation)", launch_lds<K, R>, 1, 256, false},
         {"multi CH1", launch_m<K, R, 1>, 1, 256, false},
         {"multi CH2", launch_m<K, R, 2>, 1, 256, false},
         {"multi CH4", launch_m<K, R, 4>, 1, 256, false},
@@ -171,6 +231,23 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
     ma.obj_pass = d_objs + nobj;
     g_multi_args = &ma;
 
+    {   // log/exp tables + per-(input,row) coefficient logs for the LDS ablation
+        const GF &g = gf();
+        uint8_t le[256 + 512];
+        for (int i = 0; i < 256; ++i) le[i] = g.log[i];
+        for (int i = 0; i < 512; ++i) le[256 + i] = g.exp[i];
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(c_logexp), le, sizeof(le)));
+        std::vector<uint8_t> lc(K * R);
+        for (int c = 0; c < K; ++c)
+            for (int r = 0; r < R; ++r) {
+                const uint8_t cf = plan.coef[(size_t)r * K + c];
+                lc[c * R + r] = cf == 0 ? 255 : g.log[cf];
+            }
+        uint8_t *d_lc;
+        CK(hipMalloc(&d_lc, lc.size()));
+        CK(hipMemcpy(d_lc, lc.data(), lc.size(), hipMemcpyHostToDevice));
+        g_logc = d_lc;
+    }
     hipStream_t st;
     CK(hipStreamCreate(&st));
     std::vector<Variant> vs = variants<K, R>();
