@@ -94,6 +94,7 @@ struct rsgpu_ctx {
     std::map<std::string, std::shared_ptr<Plan>> plans;
     std::vector<std::unique_ptr<Slot>> free_slots;
     int dev_state = 0;  // 0 unknown, 1 ok, <0 error code
+    static constexpr size_t kMaxCached = 8192;  // plans / inverses kept per context
 
     const uint8_t *row(int r) const { return &m[(size_t)r * k]; }
 
@@ -123,6 +124,7 @@ struct rsgpu_ctx {
         inv.assign((size_t)k * k, 0);
         if (!gf_invert(sub.data(), k, inv.data())) return RSGPU_ERR_SINGULAR;
         std::lock_guard<std::mutex> g(mu);
+        if (inverses.size() >= kMaxCached) inverses.clear();  // bound memory under random patterns
         inverses.emplace(key, inv);
         return RSGPU_OK;
     }
@@ -135,6 +137,10 @@ struct rsgpu_ctx {
     std::shared_ptr<Plan> remember(const std::string &key, std::shared_ptr<Plan> p) {
         p->build_tables();
         std::lock_guard<std::mutex> g(mu);
+        // bound memory: upstream's inversionTree keeps every pattern, but a
+        // 256-shard code has far more patterns than are worth caching.  Plans
+        // are shared_ptr, so launches holding one keep it alive.
+        if (plans.size() >= kMaxCached) plans.clear();
         return plans.emplace(key, std::move(p)).first->second;
     }
 

@@ -61,11 +61,15 @@ struct MultiWorkspace {
     struct Slot {
         void *d = nullptr, *h = nullptr;
         size_t cap = 0;
-        hipEvent_t done = nullptr;
+        hipEvent_t done = nullptr;      // kernels that read this image finished
+        hipEvent_t uploaded = nullptr;  // the image's H2D finished
     };
     std::mutex mu;
     Slot slot[kRing];
     unsigned next = 0;
+    // images go up on their own stream so the copy overlaps whatever the
+    // caller's stream is still running (e.g. the previous kernel)
+    hipStream_t upload = nullptr;
     ~MultiWorkspace();
 };
 

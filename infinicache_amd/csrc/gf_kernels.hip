@@ -366,7 +366,9 @@ hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
 }
 
 MultiWorkspace::~MultiWorkspace() {
+    if (upload) (void)hipStreamDestroy(upload);
     for (auto &s : slot) {
+        if (s.uploaded) (void)hipEventDestroy(s.uploaded);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.d) (void)hipFree(s.d);
         if (s.h) (void)hipHostFree(s.h);
@@ -408,11 +410,16 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
     std::lock_guard<std::mutex> g(ws.mu);
     MultiWorkspace::Slot &w = ws.slot[ws.next++ % MultiWorkspace::kRing];
     hipError_t e = hipSuccess;
+    if (!ws.upload) {
+        e = hipStreamCreateWithFlags(&ws.upload, hipStreamNonBlocking);
+        if (e != hipSuccess) return e;
+    }
     if (w.done) {  // the kernels that read this image kRing calls ago must be done
         e = hipEventSynchronize(w.done);
         if (e != hipSuccess) return e;
     } else {
         e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&w.uploaded, hipEventDisableTiming);
         if (e != hipSuccess) return e;
     }
     if (w.cap < img.size()) {
@@ -428,7 +435,9 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
         w.cap = cap;
     }
     std::memcpy(w.h, img.data(), img.size());
-    e = hipMemcpyAsync(w.d, w.h, img.size(), hipMemcpyHostToDevice, st);
+    e = hipMemcpyAsync(w.d, w.h, img.size(), hipMemcpyHostToDevice, ws.upload);
+    if (e == hipSuccess) e = hipEventRecord(w.uploaded, ws.upload);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, w.uploaded, 0);
     for (auto &l : launches)
         if (e == hipSuccess) e = l.second((const uint8_t *)w.d, st);
     if (e == hipSuccess) e = hipEventRecord(w.done, st);

@@ -25,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rsgpu.h"
@@ -144,6 +145,7 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         while (j < rows.size() && rows[j] == rows[j - 1] + 1) ++j;
         const size_t off = (size_t)rows[i] * pitch, len = (size_t)(rows[j - 1] - rows[i]) * pitch + vec_bytes;
         if (hipMemcpyAsync(s->d + off, s->h + off, len, hipMemcpyHostToDevice, s->stream) != hipSuccess) {
+            (void)hipStreamSynchronize(s->stream);  // nothing in flight may touch a pooled slot
             ctx->put_slot(std::move(s));
             return RSGPU_ERR_HIP;
         }
@@ -161,6 +163,7 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         he = hipMemcpyAsync(s->h_bad, s->d_bad, 4, hipMemcpyDeviceToHost, s->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
     if (he != hipSuccess) {
+        (void)hipStreamSynchronize(s->stream);
         ctx->put_slot(std::move(s));
         return hip_fail(he, "run_host");
     }
@@ -440,32 +443,45 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
     const int n = ctx->n;
-    std::map<std::string, int> idx;
+    // pattern key: the present bitmask (n <= 64: one word; else a byte string)
+    std::unordered_map<uint64_t, int> idx64;
+    std::map<std::string, int> idx_str;
     std::vector<std::shared_ptr<Plan>> owned;
     std::vector<Plan *> plans;
     std::vector<int> plan_of(nobj, -1);
     bool any_checks = false;
     for (int o = 0; o < nobj; ++o) {
         const uint8_t *pr = present + (size_t)o * n;
-        std::string key(n, '0');
+        uint64_t mask = 0;
         int np = 0;
         for (int i = 0; i < n; ++i) {
-            key[i] = pr[i] ? '1' : '0';
-            np += pr[i] != 0;
+            if (pr[i]) {
+                ++np;
+                if (i < 64) mask |= 1ull << i;
+            }
         }
         if (np < ctx->k) return RSGPU_ERR_TOO_FEW_SHARDS;
         if (np == n && !check) continue;  // nothing to reconstruct
-        auto it = idx.find(key);
-        if (it == idx.end()) {
+        int *slot_idx;
+        if (n <= 64) {
+            auto ins = idx64.emplace(mask, -1);
+            slot_idx = &ins.first->second;
+        } else {
+            std::string key(n, '0');
+            for (int i = 0; i < n; ++i) key[i] = pr[i] ? '1' : '0';
+            auto ins = idx_str.emplace(key, -1);
+            slot_idx = &ins.first->second;
+        }
+        if (*slot_idx < 0) {
             std::shared_ptr<Plan> p;
             if (np == n) p = ctx->plan_verify();
             else if ((e = ctx->plan_reconstruct(pr, data_only, check, p))) return e;
             any_checks |= p->nw < p->R;
-            it = idx.emplace(key, (int)plans.size()).first;
+            *slot_idx = (int)plans.size();
             owned.push_back(p);
             plans.push_back(p.get());
         }
-        plan_of[o] = it->second;
+        plan_of[o] = *slot_idx;
     }
     if ((e = ctx->use_device())) return e;
     if (check && any_checks)
