@@ -1,0 +1,110 @@
+/* c_abi_client.c — a plain-C consumer of include/rsgpu.h, exercising the
+ * boundary the way the cgo shim would: create, per-object
+ * Encode / Verify / Reconstruct / decode with caller-owned host buffers,
+ * error codes.  Built by tests/test_c_abi.py with gcc against librsgpu.so and
+ * the CPU oracle (oracle/liboracle.so, the checker).
+ *
+ *   ./c_abi_client host      # no device needed: create/matrix/error paths
+ *   ./c_abi_client gpu       # + compute, checked byte-for-byte vs the oracle
+ * Exit code 0 = pass. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "rsgpu.h"
+
+/* oracle entry points (oracle/rs_oracle.c) */
+int orc_build_matrix(int k, int p, int kind, uint8_t *out);
+int orc_encode(int k, int p, int kind, uint8_t *const *shards, const size_t *lens, int nshards);
+
+#define CHECK(c)                                                         \
+    do {                                                                 \
+        if (!(c)) {                                                      \
+            fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            return 1;                                                    \
+        }                                                                \
+    } while (0)
+
+static uint64_t rng = 0x1F1C;
+static uint8_t rnd8(void) {
+    rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint8_t)(rng >> 56);
+}
+
+static int host_checks(void) {
+    rsgpu_ctx *ctx = NULL;
+    CHECK(rsgpu_create(0, 2, 0, 0, &ctx) == RSGPU_ERR_INV_SHARD_NUM && ctx == NULL);
+    CHECK(rsgpu_create(200, 57, 0, 0, &ctx) == RSGPU_ERR_MAX_SHARD_NUM);
+    CHECK(rsgpu_create(10, 2, 0, 99, &ctx) == RSGPU_ERR_INVALID_ARG);
+    CHECK(rsgpu_create(10, 2, 0, RSGPU_MATRIX_VANDERMONDE, &ctx) == RSGPU_OK && ctx);
+    CHECK(rsgpu_data_shards(ctx) == 10 && rsgpu_parity_shards(ctx) == 2);
+    uint8_t m[12 * 10], want[12 * 10];
+    CHECK(rsgpu_matrix(ctx, m) == RSGPU_OK);
+    CHECK(orc_build_matrix(10, 2, 0, want) == 0);
+    CHECK(memcmp(m, want, sizeof m) == 0);
+    /* upstream error precedence, no device needed */
+    uint8_t a[8] = {0};
+    uint8_t *sh[12];
+    size_t lens[12];
+    for (int i = 0; i < 12; i++) { sh[i] = a; lens[i] = 8; }
+    CHECK(rsgpu_encode(ctx, sh, lens, 11) == RSGPU_ERR_TOO_FEW_SHARDS);
+    lens[11] = 0;
+    CHECK(rsgpu_encode(ctx, sh, lens, 12) == RSGPU_ERR_SHARD_SIZE);
+    int ok = 7;
+    CHECK(rsgpu_verify(ctx, (const uint8_t *const *)sh, lens, 12, &ok) == RSGPU_ERR_SHARD_SIZE && ok == 0);
+    for (int i = 0; i < 12; i++) lens[i] = 0;
+    CHECK(rsgpu_encode(ctx, sh, lens, 12) == RSGPU_ERR_SHARD_NO_DATA);
+    for (int i = 0; i < 12; i++) lens[i] = i < 9 ? 8 : 0;
+    CHECK(rsgpu_reconstruct(ctx, sh, lens, 12, 0) == RSGPU_ERR_TOO_FEW_SHARDS);
+    CHECK(strlen(rsgpu_strerror(RSGPU_ERR_SHARD_SIZE)) > 0);
+    rsgpu_destroy(ctx);
+    printf("host checks ok (devices: %d)\n", rsgpu_device_count());
+    return 0;
+}
+
+static int gpu_checks(void) {
+    const int k = 10, p = 4, n = 14;
+    const size_t S = 104858;  /* 1 MiB object / 10, as Split makes it */
+    rsgpu_ctx *ctx;
+    CHECK(rsgpu_create(k, p, 0, 0, &ctx) == RSGPU_OK);
+    CHECK(rsgpu_device_ok(0) == 1);
+    uint8_t *mine[14], *ref[14];
+    size_t lens[14];
+    for (int i = 0; i < n; i++) {
+        mine[i] = malloc(S);
+        ref[i] = malloc(S);
+        lens[i] = S;
+        for (size_t j = 0; j < S; j++) mine[i][j] = ref[i][j] = i < k ? rnd8() : 0;
+    }
+    CHECK(rsgpu_encode(ctx, mine, lens, n) == RSGPU_OK);
+    CHECK(orc_encode(k, p, 0, ref, lens, n) == 0);
+    for (int i = k; i < n; i++) CHECK(memcmp(mine[i], ref[i], S) == 0);
+    int ok = 0;
+    CHECK(rsgpu_verify(ctx, (const uint8_t *const *)mine, lens, n, &ok) == RSGPU_OK && ok == 1);
+    mine[12][S - 1] ^= 1;
+    CHECK(rsgpu_verify(ctx, (const uint8_t *const *)mine, lens, n, &ok) == RSGPU_OK && ok == 0);
+    mine[12][S - 1] ^= 1;
+    /* lose data 0, 7 and parity 11: buffers supplied by the caller, len 0 */
+    int lost[3] = {0, 7, 11};
+    for (int j = 0; j < 3; j++) { memset(mine[lost[j]], 0xEE, S); lens[lost[j]] = 0; }
+    CHECK(rsgpu_reconstruct(ctx, mine, lens, n, 0) == RSGPU_OK);
+    for (int i = 0; i < n; i++) CHECK(memcmp(mine[i], ref[i], S) == 0);
+    /* fused Client.decode with one extra present shard corrupted */
+    for (int i = 0; i < n; i++) lens[i] = S;
+    lens[3] = 0;
+    memset(mine[3], 0, S);
+    mine[13][5] ^= 0x10;  /* 13 present: survivors 0..12 except 3, extra = 13 */
+    CHECK(rsgpu_decode(ctx, mine, lens, n, &ok) == RSGPU_OK && ok == 0);
+    CHECK(memcmp(mine[3], ref[3], S) == 0);
+    for (int i = 0; i < n; i++) { free(mine[i]); free(ref[i]); }
+    rsgpu_destroy(ctx);
+    printf("gpu checks ok (RS(10+4), S=%zu, bit-exact vs oracle)\n", S);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (host_checks()) return 1;
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_checks();
+    return 0;
+}

@@ -1,0 +1,40 @@
+"""Builds tests/c_abi_client.c with gcc against librsgpu.so (+ the oracle as
+the checker) and runs it: the C ABI consumed from plain C, as the cgo shim in
+INTEGRATION.md would (no Python, no torch in the process)."""
+import os
+import subprocess
+
+import pytest
+
+from infinicache_amd import _lib
+import oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+@pytest.fixture(scope="module")
+def client_bin(tmp_path_factory):
+    oracle.build()
+    out = str(tmp_path_factory.mktemp("cabi") / "c_abi_client")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    odir = os.path.join(ROOT, "oracle")
+    subprocess.check_call([
+        "gcc", "-O2", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+        os.path.join(HERE, "c_abi_client.c"), "-o", out,
+        "-L", libdir, "-lrsgpu", "-Wl,-rpath," + libdir,
+        "-L", odir, "-l:liboracle.so", "-Wl,-rpath," + odir, "-lpthread"])
+    return out
+
+
+def test_c_abi_host_paths(client_bin):
+    r = subprocess.run([client_bin], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "host checks ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_c_abi_gpu_paths(gpu, client_bin):
+    r = subprocess.run([client_bin, "gpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "gpu checks ok" in r.stdout
