@@ -10,6 +10,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rsgpu.h"
@@ -178,8 +179,34 @@ struct rsgpu_ctx {
     // the survivors becomes a check row (M[j] x inv) x survivors XOR row_j:
     // exactly the comparisons upstream's Verify-after-Reconstruct can fail;
     // the survivors' own comparisons are identities (M[V] x inv = I).
+    // fast path for n <= 64: plans keyed by (mode, present bitmask)
+    std::unordered_map<uint64_t, std::shared_ptr<Plan>> fast_plans[3];
+
     int plan_reconstruct(const uint8_t *present, bool data_only, bool check,
                          std::shared_ptr<Plan> &out) {
+        const int mode = check ? 2 : (data_only ? 1 : 0);
+        uint64_t mask = 0;
+        if (n <= 64) {
+            for (int i = 0; i < n; ++i)
+                if (present[i]) mask |= 1ull << i;
+            std::lock_guard<std::mutex> g(mu);
+            auto it = fast_plans[mode].find(mask);
+            if (it != fast_plans[mode].end()) {
+                out = it->second;
+                return RSGPU_OK;
+            }
+        }
+        int e = plan_reconstruct_slow(present, data_only, check, out);
+        if (e == RSGPU_OK && n <= 64) {
+            std::lock_guard<std::mutex> g(mu);
+            if (fast_plans[mode].size() >= kMaxCached) fast_plans[mode].clear();
+            fast_plans[mode].emplace(mask, out);
+        }
+        return e;
+    }
+
+    int plan_reconstruct_slow(const uint8_t *present, bool data_only, bool check,
+                              std::shared_ptr<Plan> &out) {
         std::string key = check ? "D" : (data_only ? "d" : "R");
         for (int i = 0; i < n; ++i) key.push_back(present[i] ? '1' : '0');
         if ((out = cached(key))) return RSGPU_OK;

@@ -42,6 +42,9 @@ struct Plan {
     uint32_t *d_in_row = nullptr;  // [K]
     std::once_flag dev_once;
     hipError_t dev_err = hipSuccess;
+    // serialized Pass images for mixed-pattern launches, per (pitch, first row)
+    std::mutex img_mu;
+    std::vector<std::pair<std::pair<size_t, int>, std::vector<uint8_t>>> pass_imgs;
     void build_tables();
     ~Plan();
 };
@@ -61,8 +64,7 @@ struct MultiWorkspace {
     struct Slot {
         void *d = nullptr, *h = nullptr;
         size_t cap = 0;
-        hipEvent_t done = nullptr;      // kernels that read this image finished
-        hipEvent_t uploaded = nullptr;  // the image's H2D finished
+        hipEvent_t done = nullptr;  // kernels that read this image finished
     };
     std::mutex mu;
     Slot slot[kRing];

@@ -203,9 +203,25 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
     img.resize(pass_off + es.size() * sizeof(Pass<K, R>));
     size_t nobj = 0;
     for (size_t i = 0; i < es.size(); ++i) {
-        Pass<K, R> pp;
-        fill_pass<K, R>(*es[i]->plan, es[i]->sub, L.pitch, nvec, d_bad != nullptr, pp);
-        std::memcpy(&img[pass_off + i * sizeof(Pass<K, R>)], &pp, sizeof(pp));
+        // the pass image depends on (plan, pitch, sub-pass, flags): cache it in the plan
+        Plan &pl = const_cast<Plan &>(*es[i]->plan);
+        const std::pair<size_t, int> key{L.pitch * 2 + (d_bad != nullptr), es[i]->sub.r0};
+        const std::vector<uint8_t> *cached = nullptr;
+        {
+            std::lock_guard<std::mutex> g(pl.img_mu);
+            for (auto &kv : pl.pass_imgs)
+                if (kv.first == key && kv.second.size() == sizeof(Pass<K, R>)) cached = &kv.second;
+            if (!cached) {
+                Pass<K, R> pp;
+                fill_pass<K, R>(pl, es[i]->sub, L.pitch, nvec, d_bad != nullptr, pp);
+                std::vector<uint8_t> b(sizeof(pp));
+                std::memcpy(b.data(), &pp, sizeof(pp));
+                if (pl.pass_imgs.size() > 16) pl.pass_imgs.clear();
+                pl.pass_imgs.emplace_back(key, std::move(b));
+                cached = &pl.pass_imgs.back().second;
+            }
+            std::memcpy(&img[pass_off + i * sizeof(Pass<K, R>)], cached->data(), sizeof(Pass<K, R>));
+        }
         nobj += es[i]->objs.size();
     }
     align();
@@ -368,7 +384,6 @@ hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
 MultiWorkspace::~MultiWorkspace() {
     if (upload) (void)hipStreamDestroy(upload);
     for (auto &s : slot) {
-        if (s.uploaded) (void)hipEventDestroy(s.uploaded);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.d) (void)hipFree(s.d);
         if (s.h) (void)hipHostFree(s.h);
@@ -419,7 +434,6 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
         if (e != hipSuccess) return e;
     } else {
         e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&w.uploaded, hipEventDisableTiming);
         if (e != hipSuccess) return e;
     }
     if (w.cap < img.size()) {
@@ -435,9 +449,11 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
         w.cap = cap;
     }
     std::memcpy(w.h, img.data(), img.size());
+    // upload on its own stream and wait for it on the HOST (~10 us for a
+    // 1024-object Get batch, while the caller's stream is still busy with
+    // earlier work): no GPU-side cross-stream dependency in front of the kernel
     e = hipMemcpyAsync(w.d, w.h, img.size(), hipMemcpyHostToDevice, ws.upload);
-    if (e == hipSuccess) e = hipEventRecord(w.uploaded, ws.upload);
-    if (e == hipSuccess) e = hipStreamWaitEvent(st, w.uploaded, 0);
+    if (e == hipSuccess) e = hipStreamSynchronize(ws.upload);
     for (auto &l : launches)
         if (e == hipSuccess) e = l.second((const uint8_t *)w.d, st);
     if (e == hipSuccess) e = hipEventRecord(w.done, st);
