@@ -192,13 +192,19 @@ def timed_run(step, steps, warmup, sync, dctx: DistCtx):
     return dctx.max(time.perf_counter() - t0)
 
 
-def pmc_traffic(kernel_key):
+def pmc_traffic(kernel_key, workload, alg_bytes):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (separate
-    --pmc passes; gfx950 FETCH_SIZE x2 correction, MI355X_MICROARCH.md §HBM)."""
+    --pmc passes; gfx950 FETCH_SIZE x2 correction, MI355X_MICROARCH.md §HBM),
+    only when that summary was taken on this same workload and launch size."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
-        return d["kernels"][kernel_key]["hbm_bytes_per_launch"]
+        if d.get("workload", "encdec") != workload:
+            return None
+        k = d["kernels"][kernel_key]
+        if k.get("algorithmic_bytes_per_launch") != alg_bytes:
+            return None
+        return k["hbm_bytes_per_launch"]
     except Exception:
         return None
 
@@ -512,7 +518,7 @@ def main():
     dom_bytes, dom_ms = per_kernel[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     kernel_key = f"gf_apply_kernel<{k},{p if dom == 'encode' else e_rows}>"
-    traffic = pmc_traffic(kernel_key)
+    traffic = pmc_traffic(kernel_key, args.workload, dom_bytes)
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 1),

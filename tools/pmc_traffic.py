@@ -41,7 +41,11 @@ def per_kernel(path, counter):
 def main():
     fetch_csv, write_csv, stats_csv, out = sys.argv[1:5]
     alg = {}
+    workload = "encdec"
     for a in sys.argv[5:]:
+        if a.startswith("--workload="):
+            workload = a.split("=", 1)[1]
+            continue
         if a.startswith("--alg"):
             continue
         k, v = a.split("=")
@@ -70,8 +74,8 @@ def main():
             d["algorithmic_bytes_per_launch"] = alg[k]
             d["traffic_over_algorithmic"] = round((rd + wr) / alg[k], 4)
         res[k] = d
-    json.dump({"note": __doc__.strip().splitlines()[0], "correction": "read = 2 x FETCH_SIZE KiB x 1024",
-               "kernels": res}, open(out, "w"), indent=1)
+    json.dump({"note": __doc__.strip().splitlines()[0], "workload": workload,
+               "correction": "read = 2 x FETCH_SIZE KiB x 1024", "kernels": res}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
