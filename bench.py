@@ -196,7 +196,9 @@ def pmc_traffic(kernel_key, workload, alg_bytes):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (separate
     --pmc passes; gfx950 FETCH_SIZE x2 correction, MI355X_MICROARCH.md §HBM),
     only when that summary was taken on this same workload and launch size."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
         if d.get("workload", "encdec") != workload:

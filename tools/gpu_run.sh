@@ -39,6 +39,11 @@ for s in $STEPS; do
             done ;;
     cpuinfo) (nproc; grep -m1 "model name" /proc/cpuinfo; grep -o -w -e avx512bw -e avx2 -e gfni /proc/cpuinfo | sort | uniq -c; cat /sys/fs/cgroup/cpu.max) > gpurun_out/cpuinfo.log 2>&1 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 ;;
+    pmc_all) for wl in enc dec4; do
+              run prof_$wl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 --workload $wl
+              run pmc_fetch_$wl 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --workload $wl
+              run pmc_write_$wl 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --workload $wl
+            done ;;
     pmc)    run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu --steps 5
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 ;;
   esac
