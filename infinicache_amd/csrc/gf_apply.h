@@ -20,12 +20,13 @@
 
 namespace rsgpu {
 
-// Kernel coefficient format: a coefficient c is stored as four u32 lookup
-// tables, one per 2-bit group g of the input byte: byte j of tab[g] is
-// c (x) (j << 2g).  Because multiplication by c is GF(2)-linear,
-// c (x) x = XOR_g tab[g][(x >> 2g) & 3], which v_perm_b32 evaluates for four
-// bytes at once.
-void coef_tables(uint8_t c, uint32_t out[4]);
+// Kernel coefficient format: a coefficient c is stored as five u32 words of
+// byte lookup tables over the bit groups [2:0], [5:3], [7:6] of the input
+// byte (layout in gf_device.h, kTabWords).  Because multiplication by c is
+// GF(2)-linear, c (x) x = c(x)(x & 7) ^ c(x)(x & 0x38) ^ c(x)(x & 0xC0), each
+// term one v_perm_b32 lookup for four bytes at once.
+constexpr int kCoefWords = 5;  // == kTabWords (gf_device.h; static_assert there)
+void coef_tables(uint8_t c, uint32_t out[kCoefWords]);
 
 struct Plan {
     int K = 0;                   // inputs
@@ -34,11 +35,11 @@ struct Plan {
     std::vector<int> in_rows;    // K row indices within an object
     std::vector<int> out_rows;   // R row indices (checked rows: unused)
     std::vector<uint8_t> coef;   // R x K
-    std::vector<uint32_t> tab;   // [R][K][4] kernel tables
+    std::vector<uint32_t> tab;   // [R][K][kCoefWords] kernel tables
     int ki = 0;                  // trailing identity inputs (gf_apply_kernel)
     // device copies for the generic (K > 16) kernel; uploaded once, then
     // immutable (safe for concurrent launches)
-    uint32_t *d_tab = nullptr;     // [K][R][4] (input-major)
+    uint32_t *d_tab = nullptr;     // [K][R][kCoefWords] (input-major)
     uint32_t *d_in_row = nullptr;  // [K]
     std::once_flag dev_once;
     hipError_t dev_err = hipSuccess;

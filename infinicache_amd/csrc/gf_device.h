@@ -12,16 +12,35 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
-__device__ __forceinline__ uint32_t lut(uint32_t t, uint32_t sel) {
-    return __builtin_amdgcn_perm(t, t, sel);
+
+// GF(2^8) multiply-by-constant c as three byte lookups on the bit groups
+// [2:0], [5:3] and [7:6] of every byte: v_perm_b32 selects any of 8 bytes
+// from its two source dwords, so one perm is a 3-bit table lookup.  A
+// coefficient's table is kTabWords dwords:
+//   t[0], t[1]: c*j, j = 0..7 (bytes 0-3, 4-7)   group [2:0]
+//   t[2], t[3]: c*(j<<3), j = 0..7               group [5:3]
+//   t[4]:       c*(j<<6), j = 0..3               group [7:6]
+// 5 VALU ops per (coefficient, dword) plus 5 per input dword for the indices,
+// vs 6 + 7 with four 2-bit groups (tools/kbench.hip).
+constexpr int kTabWords = 5;
+
+struct GfIdx {
+    uint32_t i0, i1, i2;
+};
+__device__ __forceinline__ GfIdx gf_idx(uint32_t w) {
+    return {w & 0x07070707u, (w >> 3) & 0x07070707u, (w >> 6) & 0x03030303u};
 }
 
-// acc ^= c (x) w, for one dword w whose 2-bit group indices are i0..i3.
+// v_perm_b32 byte select: 0-3 pick bytes of the second operand, 4-7 of the first
+__device__ __forceinline__ uint32_t lut8(uint32_t lo, uint32_t hi, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// acc ^= c (x) w, for one dword w with group indices g
 template <typename T>  // T: uint32_t in any address space (kernarg / constant image)
-__device__ __forceinline__ uint32_t gf_mac(uint32_t acc, T *t, uint32_t i0, uint32_t i1,
-                                           uint32_t i2, uint32_t i3) {
-    acc = xor3(acc, lut(t[0], i0), lut(t[1], i1));
-    return xor3(acc, lut(t[2], i2), lut(t[3], i3));
+__device__ __forceinline__ uint32_t gf_mac(uint32_t acc, T *t, const GfIdx &g) {
+    acc = xor3(acc, lut8(t[0], t[1], g.i0), lut8(t[2], t[3], g.i1));
+    return acc ^ lut8(t[4], t[4], g.i2);
 }
 
 // mask of the valid bytes of dword d in a 16-B vector holding `valid` bytes
@@ -41,8 +60,29 @@ struct Pass {
     uint32_t span;   // bytes addressable from an object base
     uint32_t in_off[K];
     uint32_t out_off[R];
-    uint32_t tab[K * R * 4];  // input-major [K][R][4]: one s_load_dwordx(4R) per input
+    uint32_t tab[K * R * kTabWords];  // input-major [K][R][kTabWords]: scalar loads per input
 };
+
+// Workgroup -> (item, chunk) order of a 1D launch over `total` = nitem x
+// nchunk workgroups.  The hardware deals workgroup ids round-robin to the 8
+// XCDs (id % 8), and each XCD translates through its own TLB.
+//   xper == 0: linear order (an item's chunks on consecutive ids);
+//   xper  > 0: XCD x walks the contiguous items [x*xper, (x+1)*xper), so each
+//              XCD's TLB sees 1/8 of the launch's pages.
+// The host picks xper > 0 for launches spanning more than kXcdSpan bytes
+// (past ~1.5 GiB the linear order falls from 79% to 65% of
+// HBM peak; the XCD-contiguous order recovers 3-4 points of it).
+struct Order {
+    uint32_t nchunk, total, xper;
+};
+__device__ __forceinline__ bool wg_item(const Order &o, uint32_t &item, uint32_t &chunk) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t w = o.xper ? (b & 7u) * o.xper + (b >> 3) : b;
+    if (w >= o.total) return false;
+    item = w / o.nchunk;
+    chunk = w - item * o.nchunk;
+    return true;
+}
 
 template <int K, int R>
 struct ApplyArgs {  // one pass for every object of the launch (kernarg)
@@ -51,6 +91,7 @@ struct ApplyArgs {  // one pass for every object of the launch (kernarg)
     uint32_t *bad;
     uint32_t nvec;   // 16-B vectors per row
     uint32_t tail;   // valid bytes in the last vector (1..16)
+    Order ord;       // item = object
     Pass<K, R> p;
 };
 
@@ -60,9 +101,10 @@ struct MultiArgs {  // per-object passes (a Get batch with mixed erasure pattern
     uint64_t obj_stride;
     uint32_t *bad;
     uint32_t nvec, tail;
+    Order ord;                 // item i codes object objs[i] ...
     const Pass<K, R> *passes;  // device array, one per distinct pattern
-    const uint32_t *objs;      // block y codes object objs[y] ...
-    const uint32_t *obj_pass;  // ... with passes[obj_pass[y]]
+    const uint32_t *objs;
+    const uint32_t *obj_pass;  // ... with passes[obj_pass[i]]
 };
 
 // One workgroup = BS lanes x U vectors of 16 B of one object (grid.y).
@@ -114,14 +156,10 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
             } else {
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
-                    const uint32_t w = x[u][c][d];
-                    const uint32_t i0 = w & 0x03030303u;
-                    const uint32_t i1 = (w >> 2) & 0x03030303u;
-                    const uint32_t i2 = (w >> 4) & 0x03030303u;
-                    const uint32_t i3 = (w >> 6) & 0x03030303u;
+                    const GfIdx g = gf_idx(x[u][c][d]);
 #pragma unroll
                     for (int r = 0; r < R; ++r)
-                        acc[r][d] = gf_mac(acc[r][d], &a.tab[(c * R + r) * 4], i0, i1, i2, i3);
+                        acc[r][d] = gf_mac(acc[r][d], &a.tab[(c * R + r) * kTabWords], g);
                 }
             }
             // keep the input-at-a-time order: without these fences the IR
@@ -153,9 +191,10 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
 
 template <int K, int R, int U, int BS, int LAUX, int SAUX>
 __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
-    gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)blockIdx.y * a.obj_stride, blockIdx.y,
-                                           a.p, a.nvec, a.tail, a.bad,
-                                           blockIdx.x * (BS * U) + threadIdx.x);
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec,
+                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x);
 }
 
 // Mixed erasure patterns in one launch: each workgroup reads its object's
@@ -169,13 +208,15 @@ template <int K, int R, int U, int BS, int LAUX, int SAUX, int CH>
 __global__ __launch_bounds__(BS) void gf_apply_multi(const MultiArgs<K, R> m) {
     // constant address space: the compiler may (and does) fetch the object
     // index, pass index and the pass itself with s_load (invariant, uniform)
-    const uint32_t obj = ((constant_ptr<uint32_t>)m.objs)[blockIdx.y];
-    const uint32_t pi = ((constant_ptr<uint32_t>)m.obj_pass)[blockIdx.y];
+    uint32_t item, chunk;
+    if (!wg_item(m.ord, item, chunk)) return;
+    const uint32_t obj = ((constant_ptr<uint32_t>)m.objs)[item];
+    const uint32_t pi = ((constant_ptr<uint32_t>)m.obj_pass)[item];
     const __attribute__((address_space(4))) Pass<K, R> &p = ((constant_ptr<Pass<K, R>>)m.passes)[pi];
     const uint8_t *ob = m.base + (uint64_t)obj * m.obj_stride;
     for (int ch = 0; ch < CH; ++ch)
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(ob, obj, p, m.nvec, m.tail, m.bad,
-                                               (blockIdx.x * CH + ch) * (BS * U) + threadIdx.x);
+                                               (chunk * CH + ch) * (BS * U) + threadIdx.x);
 }
 
 }  // namespace rsgpu

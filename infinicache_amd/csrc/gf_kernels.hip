@@ -5,13 +5,14 @@
 // /root/reference/client/ecRedis.go:390,395,406,415,420).
 //
 // Design:
-//   * one workgroup = 256 lanes x 16 B of one object; grid.y = object;
+//   * one workgroup = 256 lanes x 16 B of one object, 1D grid over
+//     (object, chunk) in linear or XCD-contiguous order (Order, gf_device.h);
 //   * every input row is read once with buffer_load_dwordx4 (1 KiB per wave
 //     instruction, the object base in a uniform SRD, the row offset in
 //     soffset => no per-row VALU address math);
-//   * all R outputs accumulate in VGPRs; GF multiply-by-constant is four
-//     v_perm_b32 byte lookups on 2-bit groups of the input (tables in SGPRs,
-//     from the kernarg segment) merged with v_bitop3 (3-input XOR, gfx950);
+//   * all R outputs accumulate in VGPRs; GF multiply-by-constant is three
+//     v_perm_b32 byte lookups on the 3/3/2-bit groups of the input (tables in
+//     SGPRs, from the kernarg segment) merged with v_bitop3 (3-input XOR);
 //   * rows [0, nw) are stored with buffer_store_dwordx4; rows [nw, R) are
 //     compare-to-zero rows that raise a per-object flag (fused Verify).
 // No MFMA and no LDS: the op is HBM-bound byte arithmetic.
@@ -41,22 +42,33 @@ constexpr int kUnroll = 1;     // 16-B vectors per lane
 constexpr int kLoadAux = 2;    // buffer_load: nt
 constexpr int kStoreAux = 16;  // buffer_store: sc1
 constexpr int kMultiChunks = 1; // chunks per workgroup in the mixed-pattern kernel (kbench: 1 best)
+// launches whose objects span more than this use the XCD-contiguous workgroup
+// order (gf_device.h Order; kbench footprint sweep)
+constexpr size_t kXcdSpan = (size_t)3 << 29;  // 1.5 GiB
 constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
 constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
-void coef_tables(uint8_t c, uint32_t out[4]) {
+static_assert(kTabWords == kCoefWords, "host and device table formats differ");
+
+void coef_tables(uint8_t c, uint32_t out[kCoefWords]) {
     const GF &g = gf();
-    for (int grp = 0; grp < 4; ++grp) {
+    auto pack = [&](int shift, int j0) {
         uint32_t w = 0;
-        for (int j = 0; j < 4; ++j) w |= (uint32_t)g.mul(c, (uint8_t)(j << (2 * grp))) << (8 * j);
-        out[grp] = w;
-    }
+        for (int j = 0; j < 4; ++j) w |= (uint32_t)g.mul(c, (uint8_t)((j0 + j) << shift)) << (8 * j);
+        return w;
+    };
+    out[0] = pack(0, 0);
+    out[1] = pack(0, 4);
+    out[2] = pack(3, 0);
+    out[3] = pack(3, 4);
+    out[4] = pack(6, 0);
 }
 
 void Plan::build_tables() {
-    tab.assign((size_t)R * K * 4, 0);
+    tab.assign((size_t)R * K * kTabWords, 0);
     for (int r = 0; r < R; ++r)
-        for (int c = 0; c < K; ++c) coef_tables(coef[(size_t)r * K + c], &tab[((size_t)r * K + c) * 4]);
+        for (int c = 0; c < K; ++c)
+            coef_tables(coef[(size_t)r * K + c], &tab[((size_t)r * K + c) * kTabWords]);
     // trailing identity inputs: input K-ki+j has coefficient 1 in row R-ki+j
     // and 0 in every other row
     ki = 0;
@@ -75,22 +87,25 @@ Plan::~Plan() {
 }
 
 // Generic pass for K > 16 inputs (any shard count up to 256): runtime input
-// loop, tables read by scalar loads from a device buffer laid out [K][R][4].
+// loop, tables read by scalar loads from a device buffer [K][R][kTabWords].
 struct GenericArgs {
     const uint8_t *base;
     uint64_t obj_stride;
     uint32_t *bad;
-    const uint32_t *tab;     // [K][rstride][4], pre-offset to this pass's first row
+    const uint32_t *tab;     // [K][rstride][kTabWords], pre-offset to this pass's first row
     const uint32_t *in_row;  // [K] row indices; offset = row * pitch
     uint32_t nvec, tail, nw, span, K, rstride, pitch, clear;
+    Order ord;  // item = object
     uint32_t out_off[kMaxR];
 };
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) {
-    const uint32_t v = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const uint32_t v = chunk * kBlock + threadIdx.x;
     if (v >= a.nvec) return;
-    const uint8_t *ob = a.base + (uint64_t)blockIdx.y * a.obj_stride;
+    const uint8_t *ob = a.base + (uint64_t)obj * a.obj_stride;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
     const uint32_t voff = v * 16u;
@@ -101,16 +116,12 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
         for (int d = 0; d < 4; ++d) acc[r][d] = 0;
     for (uint32_t c = 0; c < a.K; ++c) {
         const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_row[c] * a.pitch, kLoadAux);
-        const uint32_t *t = a.tab + (size_t)c * a.rstride * 4;
+        const uint32_t *t = a.tab + (size_t)c * a.rstride * kTabWords;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-            const uint32_t w = x[d];
-            const uint32_t i0 = w & 0x03030303u;
-            const uint32_t i1 = (w >> 2) & 0x03030303u;
-            const uint32_t i2 = (w >> 4) & 0x03030303u;
-            const uint32_t i3 = (w >> 6) & 0x03030303u;
+            const GfIdx g = gf_idx(x[d]);
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], t + r * 4, i0, i1, i2, i3);
+            for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], t + r * kTabWords, g);
         }
     }
     bool mismatch = false;
@@ -125,15 +136,30 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
             for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
         }
     }
-    if (mismatch) atomicOr(a.bad + blockIdx.y, 1u);
-    if (a.clear && v == 0) a.bad[blockIdx.y] = 0u;
+    if (mismatch) atomicOr(a.bad + obj, 1u);
+    if (a.clear && v == 0) a.bad[obj] = 0u;
 }
 
 // ----------------------------------------------------------------- launchers
 
 namespace {
 
-constexpr int kMaxGridY = 65535;
+// 1D launch over nitem items x nchunk workgroups; `span` = bytes the launch's
+// objects cover.  Returns the order and sets the grid size.
+Order make_order(uint32_t nchunk, uint32_t nitem, size_t span, unsigned &grid) {
+    Order o{nchunk, nchunk * nitem, 0};
+    if (span > kXcdSpan) o.xper = (o.total + 7) / 8;
+    grid = o.xper ? o.xper * 8 : o.total;
+    return o;
+}
+
+// items per launch so that the 1D grid stays below 2^31 workgroups
+int max_items(unsigned nchunk) { return (int)std::max(1u, 0x7ff00000u / std::max(1u, nchunk)); }
+
+// bytes covered by `no` objects of layout L (one object: its own span)
+size_t objs_span(const Layout &L, int no, size_t one) {
+    return no > 1 ? (size_t)no * L.obj_stride : one;
+}
 
 struct Sub {  // one pass over <= kMaxR output rows of a plan
     int r0, R, nw;
@@ -156,8 +182,8 @@ void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool ha
         a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
         maxrow = std::max(maxrow, row);
         for (int c = 0; c < K; ++c)
-            for (int g = 0; g < 4; ++g)
-                a.tab[(c * R + r) * 4 + g] = p.tab[((size_t)(s.r0 + r) * K + c) * 4 + g];
+            for (int g = 0; g < kTabWords; ++g)
+                a.tab[(c * R + r) * kTabWords + g] = p.tab[((size_t)(s.r0 + r) * K + c) * kTabWords + g];
     }
     a.span = (uint32_t)((size_t)maxrow * pitch + (size_t)nvec * 16);
 }
@@ -171,11 +197,14 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
     a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
     fill_pass<K, R>(p, s, L.pitch, a.nvec, d_bad != nullptr, a.p);
     const unsigned gx = (a.nvec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
-    for (int o0 = 0; o0 < L.nobj; o0 += kMaxGridY) {
-        const int no = std::min(kMaxGridY, L.nobj - o0);
+    const int step = max_items(gx);
+    for (int o0 = 0; o0 < L.nobj; o0 += step) {
+        const int no = std::min(step, L.nobj - o0);
         a.base = L.base + (size_t)o0 * L.obj_stride;
         a.bad = d_bad ? d_bad + o0 : nullptr;
-        hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(gx, no),
+        unsigned grid;
+        a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
+        hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
                            dim3(kBlock), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -245,12 +274,15 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
         m.passes = (const Pass<K, R> *)(dimg + pass_off);
         const unsigned per = kBlock * kUnroll * kMultiChunks;
         const unsigned gx = (nvec + per - 1) / per;
-        for (size_t o0 = 0; o0 < nobj; o0 += kMaxGridY) {
-            const int no = (int)std::min((size_t)kMaxGridY, nobj - o0);
+        const size_t step = (size_t)max_items(gx);
+        for (size_t o0 = 0; o0 < nobj; o0 += step) {
+            const int no = (int)std::min(step, nobj - o0);
             m.objs = (const uint32_t *)(dimg + objs_off) + o0;
             m.obj_pass = (const uint32_t *)(dimg + objs_off) + nobj + o0;
+            unsigned grid;
+            m.ord = make_order(gx, (uint32_t)no, objs_span(L, no, L.pitch * 256), grid);
             hipLaunchKernelGGL((gf_apply_multi<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kMultiChunks>),
-                               dim3(gx, no), dim3(kBlock), 0, st, m);
+                               dim3(grid), dim3(kBlock), 0, st, m);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -282,15 +314,15 @@ template <int R>
 hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
                           hipStream_t st) {
     const int K = p.K;
-    // upload the [K][R][4] table image and row indices once per plan
+    // upload the [K][R][kTabWords] table image and row indices once per plan
     hipError_t e = hipSuccess;
     std::call_once(p.dev_once, [&] {
-        std::vector<uint32_t> t((size_t)K * p.R * 4), rows(K);
+        std::vector<uint32_t> t((size_t)K * p.R * kTabWords), rows(K);
         for (int c = 0; c < K; ++c) {
             rows[c] = (uint32_t)p.in_rows[c];
             for (int r = 0; r < p.R; ++r)
-                for (int g = 0; g < 4; ++g)
-                    t[((size_t)c * p.R + r) * 4 + g] = p.tab[((size_t)r * K + c) * 4 + g];
+                for (int g = 0; g < kTabWords; ++g)
+                    t[((size_t)c * p.R + r) * kTabWords + g] = p.tab[((size_t)r * K + c) * kTabWords + g];
         }
         e = hipMalloc(&p.d_tab, t.size() * 4);
         if (e == hipSuccess) e = hipMalloc(&p.d_in_row, rows.size() * 4);
@@ -306,7 +338,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     a.nw = (uint32_t)s.nw;
     a.K = (uint32_t)K;
     a.rstride = (uint32_t)p.R;
-    a.tab = p.d_tab + (size_t)s.r0 * 4;
+    a.tab = p.d_tab + (size_t)s.r0 * kTabWords;
     a.in_row = p.d_in_row;
     a.pitch = (uint32_t)L.pitch;
     int maxrow = 0;
@@ -318,12 +350,15 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     }
     a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * 16);
     const unsigned gx = (a.nvec + kBlock - 1) / kBlock;
-    for (int o0 = 0; o0 < L.nobj; o0 += kMaxGridY) {
-        const int no = std::min(kMaxGridY, L.nobj - o0);
+    const int step = max_items(gx);
+    for (int o0 = 0; o0 < L.nobj; o0 += step) {
+        const int no = std::min(step, L.nobj - o0);
         a.base = L.base + (size_t)o0 * L.obj_stride;
         a.bad = d_bad ? d_bad + o0 : nullptr;
         a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
-        hipLaunchKernelGGL((gf_apply_generic<R>), dim3(gx, no), dim3(kBlock), 0, st, a);
+        unsigned grid;
+        a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
+        hipLaunchKernelGGL((gf_apply_generic<R>), dim3(grid), dim3(kBlock), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -5,6 +5,7 @@
 //   make -C tools kbench          (links ../infinicache_amd/librsgpu.so)
 //   ./tools/kbench SHAPE [rounds]
 //   SHAPE: enc10_2 | enc10_4 | dec10_2 | rdata10_4 | decx10_4 | ver10_2 | ver10_4
+//          optionally @M: M-MiB objects (e.g. enc10_2@4), xN: N objects (enc10_2x2048@1)
 //
 // Every variant's output rows are checked bit-exact against the library's own
 // launch (which the product tests pin to the oracle); check-row plans must
@@ -123,12 +124,36 @@ void launch_lds(const void *args, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((lds_logexp<K, R>), grid, dim3(256), 0, st, *(const ApplyArgs<K, R> *)args, g_logc);
 }
 
+// grid-order ablation: blockIdx.x = object, blockIdx.y = chunk (resident
+// workgroups spread over many objects instead of walking one object)
+template <int K, int R>
+__global__ __launch_bounds__(256) void apply_objmajor(const ApplyArgs<K, R> a) {
+    gf_apply_body<K, R, 1, 256, 2, 16>(a.base + (uint64_t)blockIdx.x * a.obj_stride, blockIdx.x, a.p,
+                                       a.nvec, a.tail, a.bad, blockIdx.y * 256 + threadIdx.x);
+}
+template <int K, int R>
+void launch_om(const void *args, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((apply_objmajor<K, R>), dim3(grid.y, grid.x), dim3(256), 0, st,
+                       *(const ApplyArgs<K, R> *)args);
+}
 typedef void (*launch_fn)(const void *, dim3, hipStream_t);
-template <int K, int R, int U, int BS, int LA, int SA, bool NOKI = false>
+// 1D order for a (chunks, objects) grid: ORD 0 = the library's policy
+// (XCD-contiguous past 1.5 GiB of objects), 1 = linear, 2 = XCD-contiguous
+template <int ORD>
+Order order_for(dim3 grid, size_t span, unsigned &nb) {
+    Order o{grid.x, grid.x * grid.y, 0};
+    const bool xcd = ORD == 2 || (ORD == 0 && span > ((size_t)3 << 29));
+    if (xcd) o.xper = (o.total + 7) / 8;
+    nb = o.xper ? o.xper * 8 : o.total;
+    return o;
+}
+template <int K, int R, int U, int BS, int LA, int SA, bool NOKI = false, int ORD = 0>
 void launch_v(const void *args, dim3 grid, hipStream_t st) {
     ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
     if (NOKI) a.p.ki = 0;  // every input through the dense GF path
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA>), grid, dim3(BS), 0, st, a);
+    unsigned nb;
+    a.ord = order_for<ORD>(grid, (size_t)grid.y * a.obj_stride, nb);
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA>), dim3(nb), dim3(BS), 0, st, a);
 }
 template <int K, int R>
 void launch_x(const void *args, dim3 grid, hipStream_t st) {
@@ -140,8 +165,10 @@ static const void *g_multi_args = nullptr;
 template <int K, int R, int CH>
 void launch_m(const void *, dim3 grid, hipStream_t st) {
     grid.x = (grid.x + CH - 1) / CH;
-    hipLaunchKernelGGL((gf_apply_multi<K, R, 1, 256, 2, 16, CH>), grid, dim3(256), 0, st,
-                       *(const MultiArgs<K, R> *)g_multi_args);
+    MultiArgs<K, R> m = *(const MultiArgs<K, R> *)g_multi_args;
+    unsigned nb;
+    m.ord = order_for<0>(grid, (size_t)grid.y * m.obj_stride, nb);
+    hipLaunchKernelGGL((gf_apply_multi<K, R, 1, 256, 2, 16, CH>), dim3(nb), dim3(256), 0, st, m);
 }
 
 struct Variant {
@@ -162,6 +189,9 @@ std::vector<Variant> variants() {
         {"B128 nt/sc1", launch_v<K, R, 1, 128, 2, 16>, 1, 128, false},
         {"B512 nt/sc1", launch_v<K, R, 1, 512, 2, 16>, 1, 512, false},
         {"U2 nt/sc1", launch_v<K, R, 2, 256, 2, 16>, 2, 256, false},
+        {"object-major grid", launch_om<K, R>, 1, 256, false},
+        {"order: linear", launch_v<K, R, 1, 256, 2, 16, false, 1>, 1, 256, false},
+        {"order: XCD-contiguous", launch_v<K, R, 1, 256, 2, 16, false, 2>, 1, 256, false},
         {"LDS log/exp tables (ablation)", launch_lds<K, R>, 1, 256, false},
         {"multi CH1", launch_m<K, R, 1>, 1, 256, false},
         {"multi CH2", launch_m<K, R, 2>, 1, 256, false},
@@ -205,7 +235,7 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
         a.p.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
         maxrow = std::max(maxrow, row);
         for (int c = 0; c < K; ++c)
-            for (int g = 0; g < 4; ++g) a.p.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
+            for (int g = 0; g < kTabWords; ++g) a.p.tab[(c * R + r) * kTabWords + g] = plan.tab[((size_t)r * K + c) * kTabWords + g];
     }
     a.p.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
 
@@ -354,7 +384,7 @@ int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, cons
             a.p.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * pitch);
             maxrow = std::max(maxrow, row);
             for (int c = 0; c < K; ++c)
-                for (int g = 0; g < 4; ++g) a.p.tab[(c * R + r) * 4 + g] = plan.tab[((size_t)r * K + c) * 4 + g];
+                for (int g = 0; g < kTabWords; ++g) a.p.tab[(c * R + r) * kTabWords + g] = plan.tab[((size_t)r * K + c) * kTabWords + g];
         }
         a.p.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
     }
@@ -396,10 +426,22 @@ int main(int argc, char **argv) {
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 20;
     const bool sweep = shape.rfind("pitch:", 0) == 0;  // pitch:SHAPE
     if (sweep) shape = shape.substr(6);
+    // SHAPE@M: object size M MiB (fractions allowed), launch kept near the
+    // default footprint (1 GiB of objects for 10_2, 2 GiB for 10_4)
+    double obj_mib = 0;
+    if (shape.find('@') != std::string::npos) {
+        obj_mib = std::atof(shape.substr(shape.find('@') + 1).c_str());
+        shape = shape.substr(0, shape.find('@'));
+    }
     const bool p4 = shape.find("10_4") != std::string::npos;
     const int k = 10, p = p4 ? 4 : 2, n = k + p;
-    const size_t nbytes = p4 ? (4u << 20) : (1u << 20);
-    const int nobj = p4 ? 512 : 1024;
+    if (obj_mib <= 0) obj_mib = p4 ? 4 : 1;
+    const size_t nbytes = (size_t)(obj_mib * (1 << 20));
+    int nobj = std::max(1, (int)((p4 ? 2048 : 1024) / obj_mib));
+    if (shape.find('x') != std::string::npos && shape.find('x') > shape.find('_')) {  // SHAPEx N objects
+        nobj = std::atoi(shape.substr(shape.find('x') + 1).c_str());
+        shape = shape.substr(0, shape.find('x'));
+    }
     const size_t S = (nbytes + k - 1) / k;
     rsgpu_ctx *ctx;
     if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
