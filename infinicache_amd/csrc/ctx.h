@@ -291,4 +291,8 @@ struct rsgpu_ctx {
 namespace rsgpu {
 // upstream checkShards(shards, nilok): size = first non-empty length
 int check_shards(const size_t *lens, int n, bool nilok, size_t *size);
+// true if [p, p+len) lies in one range pinned through rsgpu_host_register /
+// rsgpu_host_alloc (pipeline.cpp): the per-object host API then DMAs
+// straight from / to it instead of staging through its own pinned buffer
+bool host_pinned(const void *p, size_t len);
 }  // namespace rsgpu

@@ -43,6 +43,23 @@ __device__ __forceinline__ uint32_t gf_mac(uint32_t acc, T *t, const GfIdx &g) {
     return acc ^ lut8(t[4], t[4], g.i2);
 }
 
+// Store one 16-B output vector.  With byte-packed rows (pitch = shard size,
+// the host API's staging layout) the last vector of a row overlaps the next
+// row, so its `tail` valid bytes are stored one by one.  Rows need no 16-B
+// alignment: gfx950 buffer loads/stores honour unaligned offsets (the
+// driver's SH_MEM_CONFIG unaligned mode; tools/unaligned_probe.hip).
+template <int SAUX>
+__device__ __forceinline__ void store_row(const u32x4 &o, __amdgpu_buffer_rsrc_t rs, uint32_t voff,
+                                          uint32_t soff, bool last_packed, uint32_t tail) {
+    if (last_packed && tail < 16u) {
+        for (uint32_t b = 0; b < tail; ++b)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(o[b >> 2] >> (8 * (b & 3))), rs, voff + b, soff,
+                                                 SAUX);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, soff, SAUX);
+    }
+}
+
 // mask of the valid bytes of dword d in a 16-B vector holding `valid` bytes
 __device__ __forceinline__ uint32_t tail_mask(int d, uint32_t valid) {
     int v = (int)valid - 4 * d;
@@ -58,6 +75,7 @@ struct Pass {
     uint32_t ki;     // trailing identity inputs (see gf_apply_body)
     uint32_t clear;  // the plan has no check rows: this pass zeroes bad[obj]
     uint32_t span;   // bytes addressable from an object base
+    uint32_t packed; // rows are byte-packed (pitch % 16 != 0): see store_row
     uint32_t in_off[K];
     uint32_t out_off[R];
     uint32_t tab[K * R * kTabWords];  // input-major [K][R][kTabWords]: scalar loads per input
@@ -175,7 +193,7 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         for (int r = 0; r < R; ++r) {
             if ((uint32_t)r < a.nw) {
                 u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                __builtin_amdgcn_raw_buffer_store_b128(o, rs, v * 16u, a.out_off[r], SAUX);
+                store_row<SAUX>(o, rs, v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
             } else {
                 const uint32_t valid = (v == nvec - 1) ? tail : 16u;
 #pragma unroll

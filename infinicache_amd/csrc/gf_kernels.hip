@@ -94,7 +94,7 @@ struct GenericArgs {
     uint32_t *bad;
     const uint32_t *tab;     // [K][rstride][kTabWords], pre-offset to this pass's first row
     const uint32_t *in_row;  // [K] row indices; offset = row * pitch
-    uint32_t nvec, tail, nw, span, K, rstride, pitch, clear;
+    uint32_t nvec, tail, nw, span, K, rstride, pitch, clear, packed;
     Order ord;  // item = object
     uint32_t out_off[kMaxR];
 };
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     for (int r = 0; r < R; ++r) {
         if ((uint32_t)r < a.nw) {
             u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-            __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, a.out_off[r], kStoreAux);
+            store_row<kStoreAux>(o, rs, voff, a.out_off[r], a.packed && v == a.nvec - 1, a.tail);
         } else {
             const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
 #pragma unroll
@@ -172,6 +172,7 @@ void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool ha
     // pass is the plan's last pass (it holds those rows at the same offsets)
     a.ki = (s.r0 + R == p.R) ? (uint32_t)std::min(p.ki, R) : 0u;
     a.clear = (have_bad && p.nw == p.R) ? 1u : 0u;
+    a.packed = (pitch % 16) != 0;
     int maxrow = 0;
     for (int c = 0; c < K; ++c) {
         a.in_off[c] = (uint32_t)(p.in_rows[c] * pitch);
@@ -341,6 +342,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     a.tab = p.d_tab + (size_t)s.r0 * kTabWords;
     a.in_row = p.d_in_row;
     a.pitch = (uint32_t)L.pitch;
+    a.packed = (L.pitch % 16) != 0;
     int maxrow = 0;
     for (int c = 0; c < K; ++c) maxrow = std::max(maxrow, p.in_rows[c]);
     for (int r = 0; r < R; ++r) {

@@ -13,14 +13,16 @@
 //
 // PCIe copies are always 1D (tools/pcie_bench.hip on MI355X: a pinned 1D
 // H2D runs at 53-57 GB/s, a 2D host<->device copy with 105-KB rows at
-// 8.7 GB/s).  An object whose S is not a multiple of 16 (e.g. 104,858) is
-// therefore copied packed (pitch S) into a device staging area and repacked
-// on the device (D2D 2D copy, ~770 GB/s) to the 256-B pitch the kernel
-// needs; the parity rows go back the same way.  Host buffers should be
-// pinned (rsgpu_host_register / _alloc) for the copies to run async.
+// 8.7 GB/s).  The device image of an object is byte-packed (pitch = S, any
+// S; the pass's packed mode, gf_device.h store_row), so a Split-layout object
+// is one H2D and its parity one D2H, with no device-side repack.  Host
+// buffers should be pinned (rsgpu_host_register / _alloc) for the copies to
+// run async.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "ctx.h"
 
@@ -69,7 +71,31 @@ int drain(rsgpu_ctx *ctx) {
     return first == hipSuccess ? RSGPU_OK : hip_fail(first, "pipeline drain");
 }
 
+// ranges pinned through this API: start -> length
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;
+
+void pin_add(const void *p, size_t len) {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pinned[(uintptr_t)p] = len;
+}
+void pin_del(const void *p) {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pinned.erase((uintptr_t)p);
+}
+
 }  // namespace
+
+namespace rsgpu {
+bool host_pinned(const void *p, size_t len) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return a >= it->first && a + len <= it->first + it->second;
+}
+}  // namespace rsgpu
 
 extern "C" {
 
@@ -77,11 +103,13 @@ int rsgpu_host_register(void *p, size_t len) {
     if (!p || !len) return RSGPU_ERR_INVALID_ARG;
     if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
     HIP_TRY(hipHostRegister(p, len, hipHostRegisterDefault));
+    pin_add(p, len);
     return RSGPU_OK;
 }
 
 int rsgpu_host_unregister(void *p) {
     if (!p) return RSGPU_ERR_INVALID_ARG;
+    pin_del(p);
     HIP_TRY(hipHostUnregister(p));
     return RSGPU_OK;
 }
@@ -91,11 +119,13 @@ int rsgpu_host_alloc(size_t len, void **out) {
     *out = nullptr;
     if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
     HIP_TRY(hipHostMalloc(out, len, hipHostMallocDefault));
+    pin_add(*out, len);
     return RSGPU_OK;
 }
 
 int rsgpu_host_free(void *p) {
     if (!p) return RSGPU_OK;
+    pin_del(p);
     HIP_TRY(hipHostFree(p));
     return RSGPU_OK;
 }
@@ -107,9 +137,8 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
     for (int o = 0; o < nobj; ++o) {
         if (!objs[o]) return RSGPU_ERR_INVALID_ARG;
         if (shard_lens[o] == 0) return RSGPU_ERR_SHARD_NO_DATA;
-        // aligned image + packed staging image
-        maxbytes = std::max(maxbytes, round_up((size_t)n * round_up(shard_lens[o], 256), 256) +
-                                          (size_t)n * shard_lens[o]);
+        if ((size_t)n * shard_lens[o] >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
+        maxbytes = std::max(maxbytes, (size_t)n * shard_lens[o] + 16);
     }
     if (nobj == 0) return RSGPU_OK;
     int e = ctx->use_device();
@@ -121,18 +150,10 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
     for (int o = 0; o < nobj && he == hipSuccess; ++o) {
         PipeSlot &s = *ctx->pipe.slots[o % kSlots];
         const size_t S = shard_lens[o];
-        const bool packed = S % 16 == 0;  // rows already aligned: no repack
-        const size_t P = packed ? S : round_up(S, 256);
-        uint8_t *stage = packed ? s.d : s.d + round_up((size_t)n * P, 256);
-        he = hipMemcpyAsync(stage, objs[o], (size_t)k * S, hipMemcpyHostToDevice, s.stream);
-        if (he == hipSuccess && !packed)
-            he = hipMemcpy2DAsync(s.d, P, stage, S, S, k, hipMemcpyDeviceToDevice, s.stream);
-        if (he == hipSuccess) he = launch_plan(*plan, Layout{s.d, 0, P, S, 1}, nullptr, s.stream);
-        if (he == hipSuccess && !packed)
-            he = hipMemcpy2DAsync(stage + (size_t)k * S, S, s.d + (size_t)k * P, P, S, p,
-                                  hipMemcpyDeviceToDevice, s.stream);
+        he = hipMemcpyAsync(s.d, objs[o], (size_t)k * S, hipMemcpyHostToDevice, s.stream);
+        if (he == hipSuccess) he = launch_plan(*plan, Layout{s.d, 0, S, S, 1}, nullptr, s.stream);
         if (he == hipSuccess)
-            he = hipMemcpyAsync(objs[o] + (size_t)k * S, stage + (size_t)k * S, (size_t)p * S,
+            he = hipMemcpyAsync(objs[o] + (size_t)k * S, s.d + (size_t)k * S, (size_t)p * S,
                                 hipMemcpyDeviceToHost, s.stream);
     }
     e = drain(ctx);
@@ -158,7 +179,8 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
         int e = np == n ? (plans[o] = ctx->plan_verify(), RSGPU_OK)
                         : ctx->plan_reconstruct(pr, false, true, plans[o]);
         if (e) return e;
-        maxbytes = std::max(maxbytes, (size_t)n * round_up(shard_lens[o], 256));
+        if ((size_t)n * shard_lens[o] >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
+        maxbytes = std::max(maxbytes, (size_t)n * shard_lens[o] + 16);
     }
     if (nobj == 0) return RSGPU_OK;
     int e = ctx->use_device();
@@ -171,7 +193,7 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
         PipeSlot &s = *ctx->pipe.slots[o % kSlots];
         Plan &plan = *plans[o];
         uint8_t *const *row = shards + (size_t)o * n;
-        const size_t S = shard_lens[o], P = round_up(S, 256);
+        const size_t S = shard_lens[o], P = S;  // packed rows
         for (int c = 0; c < plan.K && he == hipSuccess; ++c)
             he = hipMemcpyAsync(s.d + (size_t)plan.in_rows[c] * P, row[plan.in_rows[c]], S,
                                 hipMemcpyHostToDevice, s.stream);

@@ -123,51 +123,85 @@ namespace {
 // Runs `plan` over one object staged from host buffers.  in_src[c] is the
 // host source of staging row plan.in_rows[c]; out_dst[r] receives written
 // row r.  Returns the mismatch flag in *bad when the plan has check rows.
+// One object through the device: inputs H2D, the plan's pass, written rows
+// D2H, the check flag.  The device image is byte-packed (row i at i*size, the
+// pass's packed mode, gf_device.h store_row), so host rows move as plain 1D
+// copies with no device-side repack:
+//   * inputs inside one range pinned with rsgpu_host_register / _alloc at
+//     base + row*size (Split's layout) go as ONE DMA of the row span;
+//   * other pinned rows go as one DMA per run of rows consecutive in both the
+//     object and host memory;
+//   * pageable rows are staged into the slot's pinned buffer (same packed
+//     layout) and go as one DMA;
+//   * written rows come back the same way (pinned: straight into the caller's
+//     buffers).
 int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
              const std::vector<const uint8_t *> &in_src, const std::vector<uint8_t *> &out_dst,
              uint32_t *bad) {
-    const size_t pitch = round_up(size, 256);
+    // row offsets are 32-bit inside the pass (Pass::in_off / out_off)
+    if ((size_t)nrows_staged * size + 16 >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
     std::unique_ptr<Slot> s;
-    int e = ctx->get_slot((size_t)nrows_staged * pitch, s);
+    int e = ctx->get_slot(round_up((size_t)nrows_staged * size + 16, 256), s);
     if (e) return e;
-    const size_t vec_bytes = round_up(size, 16);
-    // stage inputs (zero the vector tail so check rows see clean pads)
-    for (int c = 0; c < plan.K; ++c) {
-        uint8_t *dst = s->h + (size_t)plan.in_rows[c] * pitch;
-        std::memcpy(dst, in_src[c], size);
-        if (vec_bytes > size) std::memset(dst + size, 0, vec_bytes - size);
+    bool pin_in = true, pin_out = true;
+    for (int c = 0; c < plan.K && pin_in; ++c) pin_in = host_pinned(in_src[c], size);
+    for (int r = 0; r < plan.nw && pin_out; ++r) pin_out = host_pinned(out_dst[r], size);
+    int rlo = plan.in_rows[0], rhi = plan.in_rows[0];
+    for (int c = 1; c < plan.K; ++c) {
+        rlo = std::min(rlo, plan.in_rows[c]);
+        rhi = std::max(rhi, plan.in_rows[c]);
     }
-    // H2D the staged input rows, merging contiguous runs
-    std::vector<int> rows(plan.in_rows);
-    std::sort(rows.begin(), rows.end());
-    for (size_t i = 0; i < rows.size();) {
+    const size_t span = (size_t)(rhi - rlo + 1) * size;
+    // rows [i, j) of a list form a run: consecutive object rows at
+    // consecutive host addresses
+    auto run_end = [&](const std::vector<int> &rows, size_t i, auto host) {
         size_t j = i + 1;
-        while (j < rows.size() && rows[j] == rows[j - 1] + 1) ++j;
-        const size_t off = (size_t)rows[i] * pitch, len = (size_t)(rows[j - 1] - rows[i]) * pitch + vec_bytes;
-        if (hipMemcpyAsync(s->d + off, s->h + off, len, hipMemcpyHostToDevice, s->stream) != hipSuccess) {
-            (void)hipStreamSynchronize(s->stream);  // nothing in flight may touch a pooled slot
-            ctx->put_slot(std::move(s));
-            return RSGPU_ERR_HIP;
-        }
-        i = j;
-    }
+        while (j < rows.size() && rows[j] == rows[j - 1] + 1 && host(j) == host(j - 1) + size) ++j;
+        return j;
+    };
     hipError_t he = hipSuccess;
-    if (plan.nw < plan.R) he = hipMemsetAsync(s->d_bad, 0, 4, s->stream);
-    Layout L{s->d, 0, pitch, size, 1};
-    if (he == hipSuccess) he = launch_plan(plan, L, s->d_bad, s->stream);
-    for (int r = 0; r < plan.nw && he == hipSuccess; ++r) {
-        const size_t off = (size_t)plan.out_rows[r] * pitch;
-        he = hipMemcpyAsync(s->h + off, s->d + off, size, hipMemcpyDeviceToHost, s->stream);
+    const uint8_t *span0 = in_src[0] - (size_t)(plan.in_rows[0] - rlo) * size;
+    bool split = pin_in;
+    for (int c = 0; c < plan.K && split; ++c)
+        split = in_src[c] == span0 + (size_t)(plan.in_rows[c] - rlo) * size;
+    split = split && host_pinned(span0, span);
+    if (split) {
+        he = hipMemcpyAsync(s->d + (size_t)rlo * size, span0, span, hipMemcpyHostToDevice, s->stream);
+    } else if (pin_in) {
+        auto src = [&](size_t c) { return in_src[c]; };
+        for (size_t i = 0; i < (size_t)plan.K && he == hipSuccess;) {
+            const size_t j = run_end(plan.in_rows, i, src);
+            he = hipMemcpyAsync(s->d + (size_t)plan.in_rows[i] * size, in_src[i], (j - i) * size,
+                                hipMemcpyHostToDevice, s->stream);
+            i = j;
+        }
+    } else {
+        for (int c = 0; c < plan.K; ++c) std::memcpy(s->h + (size_t)plan.in_rows[c] * size, in_src[c], size);
+        he = hipMemcpyAsync(s->d + (size_t)rlo * size, s->h + (size_t)rlo * size, span, hipMemcpyHostToDevice,
+                            s->stream);
+    }
+    if (he == hipSuccess && plan.nw < plan.R) he = hipMemsetAsync(s->d_bad, 0, 4, s->stream);
+    if (he == hipSuccess) he = launch_plan(plan, Layout{s->d, 0, size, size, 1}, s->d_bad, s->stream);
+    std::vector<int> orows(plan.out_rows.begin(), plan.out_rows.begin() + plan.nw);
+    auto dst = [&](size_t r) {
+        return pin_out ? (const uint8_t *)out_dst[r] : (const uint8_t *)s->h + (size_t)orows[r] * size;
+    };
+    for (size_t i = 0; i < orows.size() && he == hipSuccess;) {
+        const size_t j = run_end(orows, i, dst);
+        he = hipMemcpyAsync((void *)dst(i), s->d + (size_t)orows[i] * size, (j - i) * size,
+                            hipMemcpyDeviceToHost, s->stream);
+        i = j;
     }
     if (he == hipSuccess && plan.nw < plan.R)
         he = hipMemcpyAsync(s->h_bad, s->d_bad, 4, hipMemcpyDeviceToHost, s->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
     if (he != hipSuccess) {
-        (void)hipStreamSynchronize(s->stream);
+        (void)hipStreamSynchronize(s->stream);  // nothing in flight may touch a pooled slot
         ctx->put_slot(std::move(s));
         return hip_fail(he, "run_host");
     }
-    for (int r = 0; r < plan.nw; ++r) std::memcpy(out_dst[r], s->h + (size_t)plan.out_rows[r] * pitch, size);
+    if (!pin_out)
+        for (int r = 0; r < plan.nw; ++r) std::memcpy(out_dst[r], s->h + (size_t)orows[r] * size, size);
     if (bad) *bad = plan.nw < plan.R ? *s->h_bad : 0;
     ctx->put_slot(std::move(s));
     return RSGPU_OK;

@@ -97,9 +97,35 @@ static int gpu_checks(void) {
     mine[13][5] ^= 0x10;  /* 13 present: survivors 0..12 except 3, extra = 13 */
     CHECK(rsgpu_decode(ctx, mine, lens, n, &ok) == RSGPU_OK && ok == 0);
     CHECK(memcmp(mine[3], ref[3], S) == 0);
+    /* pinned Split buffer (rsgpu_host_alloc): direct DMA both ways; lost
+     * shards keep their pinned buffers with len 0, as the cgo shim passes a
+     * slice with capacity */
+    uint8_t *pb = NULL;
+    CHECK(rsgpu_host_alloc(n * S, (void **)&pb) == RSGPU_OK && pb);
+    uint8_t *ps[14];
+    for (int i = 0; i < n; i++) {
+        ps[i] = pb + i * S;
+        memcpy(ps[i], i < k ? ref[i] : mine[0], S);
+        if (i >= k) memset(ps[i], 0, S);
+        lens[i] = S;
+    }
+    CHECK(rsgpu_encode(ctx, ps, lens, n) == RSGPU_OK);
+    for (int i = k; i < n; i++) CHECK(memcmp(ps[i], ref[i], S) == 0);
+    CHECK(rsgpu_verify(ctx, (const uint8_t *const *)ps, lens, n, &ok) == RSGPU_OK && ok == 1);
+    int plost[4] = {2, 3, 9, 12};
+    for (int j = 0; j < 4; j++) { memset(ps[plost[j]], 0x77, S); lens[plost[j]] = 0; }
+    CHECK(rsgpu_reconstruct(ctx, ps, lens, n, 0) == RSGPU_OK);
+    for (int i = 0; i < n; i++) CHECK(memcmp(ps[i], ref[i], S) == 0);
+    for (int i = 0; i < n; i++) lens[i] = S;
+    lens[6] = lens[7] = 0;
+    memset(ps[6], 0, S);
+    memset(ps[7], 0, S);
+    CHECK(rsgpu_decode(ctx, ps, lens, n, &ok) == RSGPU_OK && ok == 1);
+    CHECK(memcmp(ps[6], ref[6], S) == 0 && memcmp(ps[7], ref[7], S) == 0);
+    CHECK(rsgpu_host_free(pb) == RSGPU_OK);
     for (int i = 0; i < n; i++) { free(mine[i]); free(ref[i]); }
     rsgpu_destroy(ctx);
-    printf("gpu checks ok (RS(10+4), S=%zu, bit-exact vs oracle)\n", S);
+    printf("gpu checks ok (RS(10+4), S=%zu, bit-exact vs oracle, pageable and pinned)\n", S);
     return 0;
 }
 

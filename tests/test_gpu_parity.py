@@ -194,6 +194,49 @@ def test_decode_verify_fused(gpu):
     assert not enc.DecodeVerify(bad)
 
 
+@pytest.mark.parametrize("S", [104858, 8192, 1000, 17])
+def test_pinned_host_buffers(gpu, S):
+    """Host rows in ranges pinned through rsgpu_host_alloc are DMA'd directly
+    (rsgpu.cpp run_host): Split layout in one pinned buffer (contiguous runs,
+    device repack when S % 256 != 0), one pinned buffer per shard, and a mix
+    of pinned and pageable rows (staged) must all match the oracle."""
+    k, p = 10, 2
+    n = k + p
+    full = _full(k, p, S, idx=20 + S % 7)
+    enc = ia.New(k, p)
+    # Split layout, one pinned backing buffer
+    buf = ia.host_alloc(n * S)
+    sh = [buf[i * S:(i + 1) * S] for i in range(n)]
+    for i in range(k):
+        sh[i][:] = full[i]
+    for i in range(k, n):
+        sh[i][:] = 0
+    enc.Encode(sh)
+    assert all(np.array_equal(sh[i], full[i]) for i in range(n))
+    assert enc.Verify(sh)
+    sh[k + 1][S - 1] ^= 0x40
+    assert not enc.Verify(sh)
+    sh[k + 1][S - 1] ^= 0x40
+    got = [None if i in (0, 11) else sh[i] for i in range(n)]
+    enc.Reconstruct(got)
+    assert all(np.array_equal(got[i], full[i]) for i in range(n))
+    got = [None if i == 3 else sh[i] for i in range(n)]
+    assert enc.DecodeVerify(got) and np.array_equal(got[3], full[3])
+    # one pinned buffer per shard (no contiguous runs)
+    sep = [ia.host_alloc(S) for _ in range(n)]
+    for i in range(n):
+        sep[i][:] = full[i] if i < k else 0
+    enc.Encode(sep)
+    assert all(np.array_equal(sep[i], full[i]) for i in range(n))
+    got = [None if i in (1, 2) else sep[i] for i in range(n)]
+    assert enc.DecodeVerify(got)
+    assert np.array_equal(got[1], full[1]) and np.array_equal(got[2], full[2])
+    # pinned and pageable rows mixed: staged path
+    mix = [sh[i] if i % 2 else full[i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(p)]
+    enc.Encode(mix)
+    assert all(np.array_equal(mix[i], full[i]) for i in range(n))
+
+
 def test_update_matches_oracle(gpu):
     k, p, size = 10, 4, 777
     full = _full(k, p, size, idx=11)

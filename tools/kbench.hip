@@ -162,6 +162,24 @@ void launch_x(const void *args, dim3 grid, hipStream_t st) {
 
 // multi-pass variant: the same plan fetched per workgroup from device memory
 static const void *g_multi_args = nullptr;
+// the uniform kernel with its pass read from a device image through a
+// constant-address-space pointer (scalar loads) instead of the kernarg
+template <int K, int R>
+__global__ __launch_bounds__(256) void apply_cpass(const MultiArgs<K, R> m) {
+    uint32_t obj, chunk;
+    if (!wg_item(m.ord, obj, chunk)) return;
+    const __attribute__((address_space(4))) Pass<K, R> &p = *((constant_ptr<Pass<K, R>>)m.passes);
+    gf_apply_body<K, R, 1, 256, 2, 16>(m.base + (uint64_t)obj * m.obj_stride, obj, p, m.nvec, m.tail,
+                                       m.bad, chunk * 256 + threadIdx.x);
+}
+template <int K, int R>
+void launch_cp(const void *, dim3 grid, hipStream_t st) {
+    MultiArgs<K, R> m = *(const MultiArgs<K, R> *)g_multi_args;
+    unsigned nb;
+    m.ord = order_for<0>(grid, (size_t)grid.y * m.obj_stride, nb);
+    hipLaunchKernelGGL((apply_cpass<K, R>), dim3(nb), dim3(256), 0, st, m);
+}
+
 template <int K, int R, int CH>
 void launch_m(const void *, dim3 grid, hipStream_t st) {
     grid.x = (grid.x + CH - 1) / CH;
@@ -193,6 +211,7 @@ std::vector<Variant> variants() {
         {"order: linear", launch_v<K, R, 1, 256, 2, 16, false, 1>, 1, 256, false},
         {"order: XCD-contiguous", launch_v<K, R, 1, 256, 2, 16, false, 2>, 1, 256, false},
         {"LDS log/exp tables (ablation)", launch_lds<K, R>, 1, 256, false},
+        {"device pass (uniform)", launch_cp<K, R>, 1, 256, false},
         {"multi CH1", launch_m<K, R, 1>, 1, 256, false},
         {"multi CH2", launch_m<K, R, 2>, 1, 256, false},
         {"multi CH4", launch_m<K, R, 4>, 1, 256, false},
@@ -349,14 +368,14 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
 
 // Pitch sweep: the shipped variant of one plan on layouts whose row pitch is
 // roundup(S, 256) + pad, interleaved in one process (HBM channel effects).
+// One encoded buffer per pad (row pitch = roundup(S, 256) + pad) and its kernarg.
 template <int K, int R>
-int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
+int setup_bufs(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, const std::vector<size_t> &pads,
+               std::vector<uint8_t *> &bufs, std::vector<ApplyArgs<K, R>> &args, uint32_t *&bad) {
     const int n = ctx->n;
-    const size_t pads[] = {0, 256, 512, 1024, 2048, 4096, 4096 + 256, 65536 + 256};
-    const int np = sizeof(pads) / sizeof(pads[0]);
-    std::vector<uint8_t *> bufs(np);
-    std::vector<ApplyArgs<K, R>> args(np);
-    uint32_t *bad;
+    const int np = (int)pads.size();
+    bufs.assign(np, nullptr);
+    args.assign(np, ApplyArgs<K, R>());
     CK(hipMalloc(&bad, nobj * 4));
     for (int i = 0; i < np; ++i) {
         const size_t pitch = (S + 255) / 256 * 256 + pads[i], stride = n * pitch;
@@ -388,6 +407,18 @@ int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, cons
         }
         a.p.span = (uint32_t)((size_t)maxrow * pitch + (size_t)a.nvec * 16);
     }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
+
+template <int K, int R>
+int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
+    const std::vector<size_t> pads = {0, 256, 512, 1024, 2048, 4096, 4096 + 256, 65536 + 256};
+    const int np = (int)pads.size();
+    std::vector<uint8_t *> bufs;
+    std::vector<ApplyArgs<K, R>> args;
+    uint32_t *bad;
+    if (setup_bufs<K, R>(ctx, plan, S, nobj, pads, bufs, args, bad)) return 1;
     CK(hipDeviceSynchronize());
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -421,11 +452,60 @@ int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, cons
     return 0;
 }
 
+// Translation warmth: NB same-pitch buffers, each launch timed either
+// repeating one buffer (its pages' translations stay warm) or rotating
+// through all NB (every launch sweeps pages untouched for NB-1 launches),
+// in linear and XCD-contiguous workgroup order.
+template <int K, int R>
+int rot_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
+    const int NB = 4;
+    std::vector<uint8_t *> bufs;
+    std::vector<ApplyArgs<K, R>> args;
+    uint32_t *bad;
+    if (setup_bufs<K, R>(ctx, plan, S, nobj, std::vector<size_t>(NB, 0), bufs, args, bad)) return 1;
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const dim3 grid((args[0].nvec + 255) / 256, nobj);
+    const double alg = (double)nobj * (plan.K + plan.nw) * S;
+    std::printf("buffer rotation %s: K=%d R=%d S=%zu nobj=%d, %d buffers of %.2f GB\n", shape, K, R, S,
+                nobj, NB, (double)args[0].obj_stride * nobj / 1e9);
+    const char *names[4] = {"repeat, linear order", "repeat, XCD-contiguous", "rotate, linear order",
+                            "rotate, XCD-contiguous"};
+    std::vector<std::vector<float>> ms(4);
+    for (int it = 0; it < rounds + 2; ++it)
+        for (int m = 0; m < 4; ++m)
+            for (int j = 0; j < NB; ++j) {
+                const int i = m >= 2 ? j : 0;
+                CK(hipEventRecord(e0, st));
+                if (m % 2 == 0) launch_v<K, R, 1, 256, 2, 16, false, 1>(&args[i], grid, st);
+                else launch_v<K, R, 1, 256, 2, 16, false, 2>(&args[i], grid, st);
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float t;
+                CK(hipEventElapsedTime(&t, e0, e1));
+                if (it >= 2) ms[m].push_back(t);
+            }
+    for (int m = 0; m < 4; ++m) {
+        std::sort(ms[m].begin(), ms[m].end());
+        const double med = ms[m][ms[m].size() / 2];
+        std::printf("  %-24s med %8.1f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n", names[m], med * 1e3,
+                    alg / (med * 1e-3) / 1e9, 100.0 * alg / (med * 1e-3) / 8e12);
+    }
+    for (auto b : bufs) CK(hipFree(b));
+    CK(hipFree(bad));
+    return 0;
+}
+
 int main(int argc, char **argv) {
     std::string shape = argc > 1 ? argv[1] : "enc10_2";
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 20;
     const bool sweep = shape.rfind("pitch:", 0) == 0;  // pitch:SHAPE
     if (sweep) shape = shape.substr(6);
+    const bool rot = shape.rfind("rot:", 0) == 0;  // rot:SHAPE
+    if (rot) shape = shape.substr(4);
     // SHAPE@M: object size M MiB (fractions allowed), launch kept near the
     // default footprint (1 GiB of objects for 10_2, 2 GiB for 10_4)
     double obj_mib = 0;
@@ -469,6 +549,7 @@ int main(int argc, char **argv) {
 #define SHAPE(k_, r_)                                                                       \
     if (K == k_ && R == r_)                                                                 \
         return sweep ? pitch_sweep<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str())      \
+             : rot   ? rot_sweep<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str())        \
                      : run<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str());
     SHAPE(10, 2) SHAPE(10, 4) SHAPE(12, 2) SHAPE(12, 4) SHAPE(14, 4)
 #undef SHAPE

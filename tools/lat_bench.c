@@ -1,0 +1,81 @@
+/* lat_bench.c — per-object latency of the host-buffer C ABI, as the cgo shim
+ *  drives it for one EcSet / EcGet: Client.encode = Encode +
+ * Verify, Client.decode = Reconstruct + Verify (fused, rsgpu_decode), 1 MiB
+ * RS(10+2) objects, shards as Split lays them out (one contiguous buffer).
+ *
+ *   ./lat_bench [iters]
+ *
+ * Prints p50/p99 in microseconds for pageable (malloc) and pinned
+ * (rsgpu_host_alloc) buffers.  No Python in the process. */
+#define _POSIX_C_SOURCE 199309L
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "rsgpu.h"
+
+static double now_us(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static int cmp(const void *a, const void *b) {
+    double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+static double pct(double *v, int n, double p) {
+    qsort(v, n, sizeof(double), cmp);
+    int i = (int)(p * (n - 1) + 0.5);
+    return v[i];
+}
+
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 200, warm = 10;
+    const int k = 10, p = 2, n = k + p;
+    const size_t nb = 1 << 20, S = (nb + k - 1) / k;
+    rsgpu_ctx *ctx;
+    if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
+    double *te = malloc(sizeof(double) * iters), *td = malloc(sizeof(double) * iters);
+    for (int pinned = 0; pinned < 2; ++pinned) {
+        uint8_t *buf = NULL, *keep = malloc(S);
+        if (pinned) {
+            if (rsgpu_host_alloc(n * S, (void **)&buf)) return 1;
+        } else {
+            buf = malloc(n * S);
+        }
+        uint64_t x = 12345;
+        for (size_t i = 0; i < k * S; ++i) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            buf[i] = (uint8_t)(x >> 56);
+        }
+        uint8_t *sh[12];
+        size_t lens[12];
+        for (int i = 0; i < n; ++i) { sh[i] = buf + i * S; lens[i] = S; }
+        for (int it = 0; it < iters + warm; ++it) {
+            for (int i = 0; i < n; ++i) lens[i] = S;
+            double t0 = now_us();
+            int ok = 0;
+            if (rsgpu_encode(ctx, sh, lens, n)) return 2;
+            if (rsgpu_verify(ctx, (const uint8_t *const *)sh, lens, n, &ok) || !ok) return 3;
+            double t1 = now_us();
+            memcpy(keep, sh[0], S);
+            lens[0] = lens[5] = 0;
+            double t2 = now_us();
+            if (rsgpu_decode(ctx, sh, lens, n, &ok) || !ok) return 4;
+            double t3 = now_us();
+            if (memcmp(keep, sh[0], S)) { fprintf(stderr, "decode mismatch\n"); return 5; }
+            if (it >= warm) { te[it - warm] = t1 - t0; td[it - warm] = t3 - t2; }
+        }
+        printf("%-8s encode+verify p50 %7.1f us  p99 %7.1f us   decode p50 %7.1f us  p99 %7.1f us\n",
+               pinned ? "pinned" : "pageable", pct(te, iters, 0.5), pct(te, iters, 0.99), pct(td, iters, 0.5),
+               pct(td, iters, 0.99));
+        if (pinned) rsgpu_host_free(buf); else free(buf);
+        free(keep);
+    }
+    rsgpu_destroy(ctx);
+    return 0;
+}
