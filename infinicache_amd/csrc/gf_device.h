@@ -87,9 +87,8 @@ struct Pass {
 //   xper == 0: linear order (an item's chunks on consecutive ids);
 //   xper  > 0: XCD x walks the contiguous items [x*xper, (x+1)*xper), so each
 //              XCD's TLB sees 1/8 of the launch's pages.
-// The host picks xper > 0 for launches spanning more than kXcdSpan bytes
-// (past ~1.5 GiB the linear order falls from 79% to 65% of
-// HBM peak; the XCD-contiguous order recovers 3-4 points of it).
+// The host uses xper > 0 (on cold batches the XCD-contiguous
+// order runs 2-4 points of HBM peak above the linear one).
 struct Order {
     uint32_t nchunk, total, xper;
 };

@@ -32,19 +32,28 @@
 namespace rsgpu {
 
 // Tuned launch shape of the specialised pass (tools/kbench.hip sweeps on
-// MI355X): 256 lanes x one 16-B vector per row; non-temporal
-// (nt) input loads — every input byte is read exactly once, so keeping it
-// out of the caches frees them for the output write stream (59% -> 75% of
-// HBM peak); sc1 (system-scope, write-through) stores (+3-7 points on the
-// write-heavy plans, measured interleaved against sc0|sc1, nt and default).
+// MI355X), measured on COLD batches: every timed launch reads a
+// batch copy that no launch has touched within the last ~4 GB of traffic, so
+// nothing of it is still in the 256 MiB Infinity Cache (KB_ROT=4).  A batch
+// that is re-coded back to back instead (the same 1.3 GB every launch) gets
+// its parity rewrites absorbed by that cache; that warm rate is not the HBM
+// rate and is not what the policy is tuned for.
+//   * 256 lanes x one 16-B vector per row (128/512/1024 lanes, 2-4 vectors
+//     per lane and walking 2-8 chunks per workgroup are all <= this);
+//   * non-temporal (nt) input loads: every input byte is read exactly once;
+//   * nt stores: 70.1 vs 67.9 % (sc1) cold on RS(10+2) encode (sc1 wins only
+//     warm: 80 vs 70 %, the Infinity Cache absorbing repeated parity writes);
+//   * XCD-contiguous workgroup order for every launch: 72.7 vs 70.0 % (linear)
+//     cold; splitting each XCD's share into 2-32 interleaved regions loses
+//     1-9 points (gf_device.h Order).
 constexpr int kBlock = 256;    // lanes per workgroup
 constexpr int kUnroll = 1;     // 16-B vectors per lane
 constexpr int kLoadAux = 2;    // buffer_load: nt
-constexpr int kStoreAux = 16;  // buffer_store: sc1
+constexpr int kStoreAux = 2;   // buffer_store: nt
 constexpr int kMultiChunks = 1; // chunks per workgroup in the mixed-pattern kernel (kbench: 1 best)
 // launches whose objects span more than this use the XCD-contiguous workgroup
-// order (gf_device.h Order; kbench footprint sweep)
-constexpr size_t kXcdSpan = (size_t)3 << 29;  // 1.5 GiB
+// order (gf_device.h Order); 0: every launch
+constexpr size_t kXcdSpan = 0;
 constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
 constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
@@ -148,7 +157,7 @@ namespace {
 // objects cover.  Returns the order and sets the grid size.
 Order make_order(uint32_t nchunk, uint32_t nitem, size_t span, unsigned &grid) {
     Order o{nchunk, nchunk * nitem, 0};
-    if (span > kXcdSpan) o.xper = (o.total + 7) / 8;
+    if (span > kXcdSpan && o.total >= 8) o.xper = (o.total + 7) / 8;
     grid = o.xper ? o.xper * 8 : o.total;
     return o;
 }

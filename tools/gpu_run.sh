@@ -19,7 +19,7 @@ run() {  # run <name> <timeout> cmd...
 STEPS=${STEPS:-"pytest smoke bench prof"}
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ;;
     bench_all)

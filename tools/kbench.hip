@@ -128,7 +128,7 @@ void launch_lds(const void *args, dim3 grid, hipStream_t st) {
 // workgroups spread over many objects instead of walking one object)
 template <int K, int R>
 __global__ __launch_bounds__(256) void apply_objmajor(const ApplyArgs<K, R> a) {
-    gf_apply_body<K, R, 1, 256, 2, 16>(a.base + (uint64_t)blockIdx.x * a.obj_stride, blockIdx.x, a.p,
+    gf_apply_body<K, R, 1, 256, 2, 2>(a.base + (uint64_t)blockIdx.x * a.obj_stride, blockIdx.x, a.p,
                                        a.nvec, a.tail, a.bad, blockIdx.y * 256 + threadIdx.x);
 }
 template <int K, int R>
@@ -138,11 +138,14 @@ void launch_om(const void *args, dim3 grid, hipStream_t st) {
 }
 typedef void (*launch_fn)(const void *, dim3, hipStream_t);
 // 1D order for a (chunks, objects) grid: ORD 0 = the library's policy
-// (XCD-contiguous past 1.5 GiB of objects), 1 = linear, 2 = XCD-contiguous
+// (XCD-contiguous for every launch of >= 8 workgroups), 1 = linear,
+// 2 = XCD-contiguous.  (Profiles before the cold-batch retune used ORD 0 =
+// XCD-contiguous only past 1.5 GiB of objects.)
 template <int ORD>
 Order order_for(dim3 grid, size_t span, unsigned &nb) {
+    (void)span;
     Order o{grid.x, grid.x * grid.y, 0};
-    const bool xcd = ORD == 2 || (ORD == 0 && span > ((size_t)3 << 29));
+    const bool xcd = ORD == 2 || (ORD == 0 && o.total >= 8);
     if (xcd) o.xper = (o.total + 7) / 8;
     nb = o.xper ? o.xper * 8 : o.total;
     return o;
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256) void apply_cpass(const MultiArgs<K, R> m) {
     uint32_t obj, chunk;
     if (!wg_item(m.ord, obj, chunk)) return;
     const __attribute__((address_space(4))) Pass<K, R> &p = *((constant_ptr<Pass<K, R>>)m.passes);
-    gf_apply_body<K, R, 1, 256, 2, 16>(m.base + (uint64_t)obj * m.obj_stride, obj, p, m.nvec, m.tail,
+    gf_apply_body<K, R, 1, 256, 2, 2>(m.base + (uint64_t)obj * m.obj_stride, obj, p, m.nvec, m.tail,
                                        m.bad, chunk * 256 + threadIdx.x);
 }
 template <int K, int R>
@@ -186,7 +189,27 @@ void launch_m(const void *, dim3 grid, hipStream_t st) {
     MultiArgs<K, R> m = *(const MultiArgs<K, R> *)g_multi_args;
     unsigned nb;
     m.ord = order_for<0>(grid, (size_t)grid.y * m.obj_stride, nb);
-    hipLaunchKernelGGL((gf_apply_multi<K, R, 1, 256, 2, 16, CH>), dim3(nb), dim3(256), 0, st, m);
+    hipLaunchKernelGGL((gf_apply_multi<K, R, 1, 256, 2, 2, CH>), dim3(nb), dim3(256), 0, st, m);
+}
+
+// one workgroup walks CH consecutive chunks of its object (longer
+// sequential runs per DRAM page for each of the K+R row streams)
+template <int K, int R, int CH>
+__global__ __launch_bounds__(256) void apply_walk(const ApplyArgs<K, R> a) {
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const uint8_t *ob = a.base + (uint64_t)obj * a.obj_stride;
+    for (int ch = 0; ch < CH; ++ch)
+        gf_apply_body<K, R, 1, 256, 2, 2>(ob, obj, a.p, a.nvec, a.tail, a.bad,
+                                          (chunk * CH + ch) * 256 + threadIdx.x);
+}
+template <int K, int R, int CH>
+void launch_w(const void *args, dim3 grid, hipStream_t st) {
+    grid.x = (grid.x + CH - 1) / CH;
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    unsigned nb;
+    a.ord = order_for<0>(grid, (size_t)grid.y * a.obj_stride, nb);
+    hipLaunchKernelGGL((apply_walk<K, R, CH>), dim3(nb), dim3(256), 0, st, a);
 }
 
 struct Variant {
@@ -196,20 +219,121 @@ struct Variant {
     bool ceiling;
 };
 
+// memory-pattern ceiling with a chosen store policy
+template <int K, int R, int SA>
+__global__ __launch_bounds__(256) void xor_only_sa(const ApplyArgs<K, R> a) {
+    const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= a.nvec) return;
+    const uint8_t *ob = a.base + (uint64_t)blockIdx.y * a.obj_stride;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.p.span, 0x00020000);
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.p.in_off[c], 2);
+    u32x4 acc = x[0];
+#pragma unroll
+    for (int c = 1; c < K; ++c) acc ^= x[c];
+    for (uint32_t r = 0; r < a.p.nw; ++r)
+        __builtin_amdgcn_raw_buffer_store_b128(acc, rs, v * 16u, a.p.out_off[r], SA);
+    if (a.p.nw == 0 && acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) a.bad[0] = 1;  // keep live
+}
+template <int K, int R, int SA>
+void launch_xs(const void *args, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((xor_only_sa<K, R, SA>), grid, dim3(256), 0, st, *(const ApplyArgs<K, R> *)args);
+}
+
+// M sub-streams per XCD: workgroup b runs on XCD x = b % 8; its t-th turn
+// (t = b / 8) goes to region x + 8 * (t % M) at position t / M, so the launch
+// is swept as 8*M contiguous regions at once (M = 1: XCD-contiguous order)
+template <int K, int R, int M, int BS, int LA, int SA>
+__global__ __launch_bounds__(BS) void apply_regions(const ApplyArgs<K, R> a, uint32_t per) {
+    const uint32_t b = blockIdx.x, x = b & 7u, t = b >> 3;
+    const uint32_t w = (x + 8u * (t % M)) * per + t / M;
+    if (w >= a.ord.total) return;
+    const uint32_t obj = w / a.ord.nchunk, chunk = w - obj * a.ord.nchunk;
+    gf_apply_body<K, R, 1, BS, LA, SA>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec, a.tail,
+                                       a.bad, chunk * BS + threadIdx.x);
+}
+template <int K, int R, int M, int BS = 256>
+void launch_rg(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    a.ord.nchunk = grid.x;
+    a.ord.total = grid.x * grid.y;
+    const uint32_t per = (a.ord.total + 8 * M - 1) / (8 * M);
+    hipLaunchKernelGGL((apply_regions<K, R, M, BS, 2, 2>), dim3(per * 8 * M), dim3(BS), 0, st, a, per);
+}
+
+// KB_SET=order: cold-HBM sweep of the launch order with nt/nt policy
+template <int K, int R>
+std::vector<Variant> order_variants() {
+    return {
+        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"nt/sc1 (pre-retune)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
+        {"nt/nt linear", launch_v<K, R, 1, 256, 2, 2, false, 1>, 1, 256, false},
+        {"nt/nt XCD-contiguous", launch_v<K, R, 1, 256, 2, 2, false, 2>, 1, 256, false},
+        {"nt/nt regions M=1", launch_rg<K, R, 1>, 1, 256, false},
+        {"nt/nt regions M=2", launch_rg<K, R, 2>, 1, 256, false},
+        {"nt/nt regions M=4", launch_rg<K, R, 4>, 1, 256, false},
+        {"nt/nt regions M=8", launch_rg<K, R, 8>, 1, 256, false},
+        {"nt/nt regions M=32", launch_rg<K, R, 32>, 1, 256, false},
+        {"B128 nt/nt regions M=1", launch_rg<K, R, 1, 128>, 1, 128, false},
+        {"B128 nt/nt regions M=2", launch_rg<K, R, 2, 128>, 1, 128, false},
+        {"B512 nt/nt regions M=1", launch_rg<K, R, 1, 512>, 1, 512, false},
+        {"xor-only, SA nt", launch_xs<K, R, 2>, 1, 256, true},
+    };
+}
+
+// KB_SET=policy: cache-policy bits of loads (LA) and stores (SA); gfx950
+// buffer-op aux: 1 = sc0, 2 = nt, 16 = sc1
+template <int K, int R>
+std::vector<Variant> policy_variants() {
+    return {
+        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"LA nt / SA sc1 (pre-retune)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
+        {"LA nt / SA 0", launch_v<K, R, 1, 256, 2, 0>, 1, 256, false},
+        {"LA nt / SA sc0", launch_v<K, R, 1, 256, 2, 1>, 1, 256, false},
+        {"LA nt / SA nt", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"LA nt / SA sc0 nt", launch_v<K, R, 1, 256, 2, 3>, 1, 256, false},
+        {"LA nt / SA sc1 nt", launch_v<K, R, 1, 256, 2, 18>, 1, 256, false},
+        {"LA nt / SA sc0 sc1 nt", launch_v<K, R, 1, 256, 2, 19>, 1, 256, false},
+        {"LA sc0 nt / SA nt", launch_v<K, R, 1, 256, 3, 2>, 1, 256, false},
+        {"LA sc1 nt / SA nt", launch_v<K, R, 1, 256, 18, 2>, 1, 256, false},
+        {"LA sc0 sc1 nt / SA nt", launch_v<K, R, 1, 256, 19, 2>, 1, 256, false},
+        {"LA sc0 sc1 / SA nt", launch_v<K, R, 1, 256, 17, 2>, 1, 256, false},
+        {"B128 nt/nt", launch_v<K, R, 1, 128, 2, 2>, 1, 128, false},
+        {"B512 nt/nt", launch_v<K, R, 1, 512, 2, 2>, 1, 512, false},
+        {"U2 nt/nt", launch_v<K, R, 2, 256, 2, 2>, 2, 256, false},
+        {"nt/nt XCD order", launch_v<K, R, 1, 256, 2, 2, false, 2>, 1, 256, false},
+        {"nt/nt linear order", launch_v<K, R, 1, 256, 2, 2, false, 1>, 1, 256, false},
+        {"xor-only, SA sc1", launch_xs<K, R, 16>, 1, 256, true},
+        {"xor-only, SA nt", launch_xs<K, R, 2>, 1, 256, true},
+        {"xor-only, SA sc0 sc1 nt", launch_xs<K, R, 19>, 1, 256, true},
+    };
+}
+
 template <int K, int R>
 std::vector<Variant> variants() {
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "policy") return policy_variants<K, R>();
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "order") return order_variants<K, R>();
     return {
-        {"shipped(U1,B256,nt/sc1)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
-        {"no identity inputs", launch_v<K, R, 1, 256, 2, 16, true>, 1, 256, false},
+        {"shipped(U1,B256,nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"nt/sc1 (pre-retune)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
+        {"no identity inputs", launch_v<K, R, 1, 256, 2, 2, true>, 1, 256, false},
         {"nt/sc01", launch_v<K, R, 1, 256, 2, 17>, 1, 256, false},
         {"default-policy", launch_v<K, R, 1, 256, 0, 0>, 1, 256, false},
-        {"nt/nt", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
-        {"B128 nt/sc1", launch_v<K, R, 1, 128, 2, 16>, 1, 128, false},
-        {"B512 nt/sc1", launch_v<K, R, 1, 512, 2, 16>, 1, 512, false},
-        {"U2 nt/sc1", launch_v<K, R, 2, 256, 2, 16>, 2, 256, false},
+        {"B128 nt/nt", launch_v<K, R, 1, 128, 2, 2>, 1, 128, false},
+        {"B512 nt/nt", launch_v<K, R, 1, 512, 2, 2>, 1, 512, false},
+        {"U2 nt/nt", launch_v<K, R, 2, 256, 2, 2>, 2, 256, false},
+        {"U4 nt/nt", launch_v<K, R, 4, 256, 2, 2>, 4, 256, false},
+        {"B1024 nt/nt", launch_v<K, R, 1, 1024, 2, 2>, 1, 1024, false},
+        {"walk CH2", launch_w<K, R, 2>, 1, 256, false},
+        {"walk CH4", launch_w<K, R, 4>, 1, 256, false},
+        {"walk CH8", launch_w<K, R, 8>, 1, 256, false},
+        {"default loads / sc1", launch_v<K, R, 1, 256, 0, 16>, 1, 256, false},
+        {"nt / default stores", launch_v<K, R, 1, 256, 2, 0>, 1, 256, false},
         {"object-major grid", launch_om<K, R>, 1, 256, false},
-        {"order: linear", launch_v<K, R, 1, 256, 2, 16, false, 1>, 1, 256, false},
-        {"order: XCD-contiguous", launch_v<K, R, 1, 256, 2, 16, false, 2>, 1, 256, false},
+        {"order: linear", launch_v<K, R, 1, 256, 2, 2, false, 1>, 1, 256, false},
+        {"order: XCD-contiguous", launch_v<K, R, 1, 256, 2, 2, false, 2>, 1, 256, false},
         {"LDS log/exp tables (ablation)", launch_lds<K, R>, 1, 256, false},
         {"device pass (uniform)", launch_cp<K, R>, 1, 256, false},
         {"multi CH1", launch_m<K, R, 1>, 1, 256, false},
@@ -224,14 +348,24 @@ template <int K, int R>
 int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
     const int n = ctx->n;
     const size_t pitch = (S + 255) / 256 * 256, stride = n * pitch, total = stride * nobj;
+    // KB_ROT=NB: NB copies of the batch; every timed launch moves on to the
+    // next copy, so with NB*total >> 256 MiB no byte of a launch is still in
+    // the Infinity Cache from the launch before (cold-HBM rate; NB=1 repeats
+    // one batch, which a 1.3 GB sweep partly re-reads from that cache)
+    const int NB = std::max(1, std::getenv("KB_ROT") ? std::atoi(std::getenv("KB_ROT")) : 1);
+    // KB_ALLOC=1: physically contiguous allocation (hipDeviceMallocContiguous),
+    // which lets the driver map the batch with the largest page fragments
+    const int alloc = std::getenv("KB_ALLOC") ? std::atoi(std::getenv("KB_ALLOC")) : 0;
     uint8_t *d;
-    CK(hipMalloc(&d, total));
+    if (alloc == 1) CK(hipExtMallocWithFlags((void **)&d, total * NB, hipDeviceMallocContiguous));
+    else CK(hipMalloc(&d, total * NB));
+    std::printf("allocation: %s\n", alloc == 1 ? "hipExtMallocWithFlags(contiguous)" : "hipMalloc");
     uint32_t *bad;
     CK(hipMalloc(&bad, nobj * 4));
-    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, total, 12345ull);
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, total * NB, 12345ull);
     CK(hipDeviceSynchronize());
     // consistent parity for check-row plans
-    if (rsgpu_encode_dev(ctx, d, S, pitch, stride, nobj, nullptr)) return 1;
+    if (rsgpu_encode_dev(ctx, d, S, pitch, stride, nobj * NB, nullptr)) return 1;
     CK(hipDeviceSynchronize());
 
     ApplyArgs<K, R> a;
@@ -341,18 +475,23 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int it = 0; it < rounds + 3; ++it)
-        for (int v = 0; v < nv; ++v) {
-            CK(hipEventRecord(e0, st));
-            vs[v].fn(&a, grid(vs[v]), st);
-            CK(hipEventRecord(e1, st));
-            CK(hipEventSynchronize(e1));
-            float t;
-            CK(hipEventElapsedTime(&t, e0, e1));
-            if (it >= 3) ms[v].push_back(t);
-        }
+        for (int v = 0; v < nv; ++v)
+            for (int j = 0; j < NB; ++j) {
+                a.base = d + (size_t)j * total;
+                ma.base = a.base;
+                CK(hipEventRecord(e0, st));
+                vs[v].fn(&a, grid(vs[v]), st);
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float t;
+                CK(hipEventElapsedTime(&t, e0, e1));
+                if (it >= 3) ms[v].push_back(t);
+            }
     const double alg = (double)nobj * (plan.K + plan.nw) * S;
-    std::printf("shape %s: K=%d R=%d (nw=%d, ki=%d) S=%zu nobj=%d, algorithmic bytes/launch %.0f\n",
-                shape, K, R, plan.nw, plan.ki, S, nobj, alg);
+    std::printf("shape %s: K=%d R=%d (nw=%d, ki=%d) S=%zu nobj=%d, algorithmic bytes/launch %.0f, "
+                "%d rotating batch cop%s (%s)\n",
+                shape, K, R, plan.nw, plan.ki, S, nobj, alg, NB, NB > 1 ? "ies" : "y",
+                NB > 1 ? "cold Infinity Cache" : "repeat: warm Infinity Cache");
     for (int v = 0; v < nv; ++v) {
         std::vector<float> x = ms[v];
         std::sort(x.begin(), x.end());
@@ -430,7 +569,7 @@ int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, cons
     for (int it = 0; it < rounds + 3; ++it)
         for (int i = 0; i < np; ++i) {
             CK(hipEventRecord(e0, st));
-            launch_v<K, R, 1, 256, 2, 16>(&args[i], grid, st);
+            launch_v<K, R, 1, 256, 2, 2>(&args[i], grid, st);
             CK(hipEventRecord(e1, st));
             CK(hipEventSynchronize(e1));
             float t;
@@ -472,23 +611,32 @@ int rot_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const 
     const double alg = (double)nobj * (plan.K + plan.nw) * S;
     std::printf("buffer rotation %s: K=%d R=%d S=%zu nobj=%d, %d buffers of %.2f GB\n", shape, K, R, S,
                 nobj, NB, (double)args[0].obj_stride * nobj / 1e9);
-    const char *names[4] = {"repeat, linear order", "repeat, XCD-contiguous", "rotate, linear order",
-                            "rotate, XCD-contiguous"};
-    std::vector<std::vector<float>> ms(4);
+    // modes 4/5: repeat one buffer, but sweep 512 MiB of scratch writes
+    // through the Infinity Cache (256 MiB) before each timed launch, so no
+    // byte of the launch can hit in it (cold-MALL rate)
+    const char *names[6] = {"repeat, linear order", "repeat, XCD-contiguous", "rotate, linear order",
+                            "rotate, XCD-contiguous", "repeat+MALL flush, linear", "repeat+MALL flush, XCD"};
+    const size_t nflush = (size_t)512 << 20;
+    uint8_t *flush;
+    CK(hipMalloc(&flush, nflush));
+    const int NM = 6;
+    std::vector<std::vector<float>> ms(NM);
     for (int it = 0; it < rounds + 2; ++it)
-        for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < NM; ++m)
             for (int j = 0; j < NB; ++j) {
-                const int i = m >= 2 ? j : 0;
+                const int i = (m == 2 || m == 3) ? j : 0;
+                if (m >= 4) hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, st, flush, nflush, 99ull + j);
                 CK(hipEventRecord(e0, st));
-                if (m % 2 == 0) launch_v<K, R, 1, 256, 2, 16, false, 1>(&args[i], grid, st);
-                else launch_v<K, R, 1, 256, 2, 16, false, 2>(&args[i], grid, st);
+                if (m % 2 == 0) launch_v<K, R, 1, 256, 2, 2, false, 1>(&args[i], grid, st);
+                else launch_v<K, R, 1, 256, 2, 2, false, 2>(&args[i], grid, st);
                 CK(hipEventRecord(e1, st));
                 CK(hipEventSynchronize(e1));
                 float t;
                 CK(hipEventElapsedTime(&t, e0, e1));
                 if (it >= 2) ms[m].push_back(t);
             }
-    for (int m = 0; m < 4; ++m) {
+    CK(hipFree(flush));
+    for (int m = 0; m < NM; ++m) {
         std::sort(ms[m].begin(), ms[m].end());
         const double med = ms[m][ms[m].size() / 2];
         std::printf("  %-24s med %8.1f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n", names[m], med * 1e3,
