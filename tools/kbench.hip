@@ -217,7 +217,51 @@ struct Variant {
     launch_fn fn;
     int U, BS;
     bool ceiling;
+    int rd = -1, wr = -1;  // rows read / written per object (-1: the plan's K / nw)
 };
+
+// stream probes for KB_SET=stream: the plan's K input rows read and nothing
+// written, or W rows written (rows 0..W-1 of the object) and nothing read
+template <int K, int R>
+__global__ __launch_bounds__(256) void stream_read(const ApplyArgs<K, R> a) {
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const uint32_t v = chunk * 256 + threadIdx.x;
+    if (v >= a.nvec) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)obj * a.obj_stride), (short)0, (int)a.p.span, 0x00020000);
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < K; ++c) acc ^= __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.p.in_off[c], 2);
+    if (acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u && acc[2] == 7u) a.bad[0] = 1;  // keep live
+}
+template <int K, int R, int W>
+__global__ __launch_bounds__(256) void stream_write(const ApplyArgs<K, R> a, uint32_t pitch) {
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const uint32_t v = chunk * 256 + threadIdx.x;
+    if (v >= a.nvec) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)obj * a.obj_stride), (short)0, (int)a.p.span, 0x00020000);
+    const u32x4 o = {v, obj, v ^ obj, 0x5a5a5a5au};
+#pragma unroll
+    for (int r = 0; r < W; ++r) __builtin_amdgcn_raw_buffer_store_b128(o, rs, v * 16u, r * pitch, 2);
+}
+static uint32_t g_pitch = 0;
+template <int K, int R>
+void launch_sr(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    hipLaunchKernelGGL((stream_read<K, R>), dim3(nb), dim3(256), 0, st, a);
+}
+template <int K, int R, int W>
+void launch_sw(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    hipLaunchKernelGGL((stream_write<K, R, W>), dim3(nb), dim3(256), 0, st, a, g_pitch);
+}
 
 // memory-pattern ceiling with a chosen store policy
 template <int K, int R, int SA>
@@ -311,8 +355,113 @@ std::vector<Variant> policy_variants() {
     };
 }
 
+// Two-phase coding (KB_SET=twophase): the write stream costs ~13 % more mixed
+// with the read stream than the two cost separately (KB_SET=stream).  Phase A
+// reads a sub-batch's input rows from HBM and writes its outputs into a small
+// scratch ring (SB objects x nw rows, kept in the 256 MiB Infinity Cache by
+// sc1 stores, re-dirtied every sub-batch); phase B copies the ring to the real
+// output rows (Infinity-Cache reads, nt HBM writes).  DRAM then sees a
+// read-only stream and a write-only stream in turn.
+static uint8_t *g_scr = nullptr;
+template <int K, int R, int SA>
+__global__ __launch_bounds__(256) void phase_a(const ApplyArgs<K, R> a, uint8_t *scr, uint32_t pitch) {
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const uint32_t v = chunk * 256 + threadIdx.x;
+    if (v >= a.nvec) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)obj * a.obj_stride), (short)0, (int)a.p.span, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(scr + (uint64_t)obj * R * pitch), (short)0, (int)(R * pitch), 0x00020000);
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.p.in_off[c], 2);
+    uint32_t acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const GfIdx g = gf_idx(x[c][d]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], &a.p.tab[(c * R + r) * kTabWords], g);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+        __builtin_amdgcn_raw_buffer_store_b128(o, ro, v * 16u, r * pitch, SA);
+    }
+}
+template <int K, int R, int LA>
+__global__ __launch_bounds__(256) void phase_b(const ApplyArgs<K, R> a, const uint8_t *scr, uint32_t pitch) {
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const uint32_t v = chunk * 256 + threadIdx.x;
+    if (v >= a.nvec) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)obj * a.obj_stride), (short)0, (int)a.p.span, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(scr + (uint64_t)obj * R * pitch), (short)0, (int)(R * pitch), 0x00020000);
+    u32x4 o[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) o[r] = __builtin_amdgcn_raw_buffer_load_b128(ri, v * 16u, r * pitch, LA);
+#pragma unroll
+    for (int r = 0; r < R; ++r) __builtin_amdgcn_raw_buffer_store_b128(o[r], rs, v * 16u, a.p.out_off[r], 2);
+    if (a.p.clear && v == 0) a.bad[obj] = 0u;
+}
+template <int K, int R, int SB, int SA, int LA>
+void launch_2p(const void *args, dim3 grid, hipStream_t st) {
+    const int nobj = (int)grid.y;
+    for (int o0 = 0; o0 < nobj; o0 += SB) {
+        ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+        a.base += (size_t)o0 * a.obj_stride;
+        a.bad += o0;
+        const dim3 g(grid.x, std::min(SB, nobj - o0));
+        unsigned nb;
+        a.ord = order_for<0>(g, 0, nb);
+        hipLaunchKernelGGL((phase_a<K, R, SA>), dim3(nb), dim3(256), 0, st, a, g_scr, g_pitch);
+        hipLaunchKernelGGL((phase_b<K, R, LA>), dim3(nb), dim3(256), 0, st, a, (const uint8_t *)g_scr, g_pitch);
+    }
+}
+template <int K, int R>
+std::vector<Variant> twophase_variants() {
+    return {
+        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"2-phase SB=64 sc1", launch_2p<K, R, 64, 16, 16>, 1, 256, false},
+        {"2-phase SB=128 sc1", launch_2p<K, R, 128, 16, 16>, 1, 256, false},
+        {"2-phase SB=256 sc1", launch_2p<K, R, 256, 16, 16>, 1, 256, false},
+        {"2-phase SB=512 sc1", launch_2p<K, R, 512, 16, 16>, 1, 256, false},
+        {"2-phase SB=256 default", launch_2p<K, R, 256, 0, 0>, 1, 256, false},
+        {"2-phase SB=256 sc0sc1", launch_2p<K, R, 256, 17, 17>, 1, 256, false},
+        {"read-only, K rows", launch_sr<K, R>, 1, 256, true, K, 0},
+        {"write-only, nw rows", launch_sw<K, R, R>, 1, 256, true, 0, R},
+    };
+}
+
+template <int K, int R>
+std::vector<Variant> stream_variants() {
+    return {
+        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"read-only, K rows", launch_sr<K, R>, 1, 256, true, K, 0},
+        {"write-only, 2 rows", launch_sw<K, R, 2>, 1, 256, true, 0, 2},
+        {"write-only, 12 rows", launch_sw<K, R, 12>, 1, 256, true, 0, 12},
+        {"xor-only (same streams)", launch_xs<K, R, 2>, 1, 256, true},
+    };
+}
+
 template <int K, int R>
 std::vector<Variant> variants() {
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "stream") return stream_variants<K, R>();
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "twophase") return twophase_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "policy") return policy_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "order") return order_variants<K, R>();
     return {
@@ -353,6 +502,8 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
     // the Infinity Cache from the launch before (cold-HBM rate; NB=1 repeats
     // one batch, which a 1.3 GB sweep partly re-reads from that cache)
     const int NB = std::max(1, std::getenv("KB_ROT") ? std::atoi(std::getenv("KB_ROT")) : 1);
+    g_pitch = (uint32_t)pitch;
+    CK(hipMalloc(&g_scr, (size_t)512 * R * pitch));  // two-phase scratch ring (<= 512 objects)
     // KB_ALLOC=1: physically contiguous allocation (hipDeviceMallocContiguous),
     // which lets the driver map the batch with the largest page fragments
     const int alloc = std::getenv("KB_ALLOC") ? std::atoi(std::getenv("KB_ALLOC")) : 0;
@@ -496,9 +647,12 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
         std::vector<float> x = ms[v];
         std::sort(x.begin(), x.end());
         const double med = x[x.size() / 2];
+        const double vb = (vs[v].rd < 0 && vs[v].wr < 0)
+                              ? alg
+                              : (double)nobj * (vs[v].rd + vs[v].wr) * S;  // this variant's own bytes
         std::printf("  %-26s med %8.1f us  best %8.1f us  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n",
-                    vs[v].name.c_str(), med * 1e3, x[0] * 1e3, alg / (med * 1e-3) / 1e9,
-                    100.0 * alg / (med * 1e-3) / 8e12, status[v].c_str());
+                    vs[v].name.c_str(), med * 1e3, x[0] * 1e3, vb / (med * 1e-3) / 1e9,
+                    100.0 * vb / (med * 1e-3) / 8e12, status[v].c_str());
     }
     CK(hipFree(d));
     CK(hipFree(bad));
