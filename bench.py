@@ -362,8 +362,7 @@ def run_latency(args):
             else:
                 sh = enc.Split(o)
             t0 = time.perf_counter()
-            enc.Encode(sh)
-            ok = enc.Verify(sh)
+            ok = enc.EncodeVerify(sh)  # Client.encode's Encode+Verify, one round trip
             t1 = time.perf_counter()
             assert ok
             got = [None if i in (0, 5) else sh[i] for i in range(k + p)]

@@ -92,6 +92,15 @@ int rsgpu_encode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
 int rsgpu_verify(rsgpu_ctx *ctx, const uint8_t *const *shards, const size_t *lens, int nshards,
                  int *ok);
 
+/* Client.encode's Encode -> Verify pair (ecRedis.go:390-395), fused: the data
+ * shards go to the device once, Encode's pass writes the parity shards back
+ * into the caller's buffers, and Verify's pass then re-checks every parity
+ * shard against the data on the same device image (the bytes just copied
+ * back) -> *ok.  Argument checks and errors are Encode's.  Saves Verify's
+ * second upload of all data+parity shards. */
+int rsgpu_encode_verify(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
+                        int *ok);
+
 /* Reconstruct / ReconstructData (upstream reconstruct(shards, dataOnly);
  * ecRedis.go:415).  lens[i] == 0 marks shard i missing; for every missing
  * shard the caller passes a writable buffer of the common shard size in

@@ -22,6 +22,7 @@ EXPORTS = (
     "rsgpu_reconstruct_dev", "rsgpu_decode_dev", "rsgpu_reconstruct_dev_multi",
     "rsgpu_decode_dev_multi", "rsgpu_encode_batch", "rsgpu_decode_batch",
     "rsgpu_host_register", "rsgpu_host_unregister", "rsgpu_host_alloc", "rsgpu_host_free",
+    "rsgpu_encode_verify",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -71,6 +72,7 @@ def load():
     L.rsgpu_device_ok.argtypes = [ci]
     L.rsgpu_encode.argtypes = [vp, u8pp, szp, ci]
     L.rsgpu_verify.argtypes = [vp, u8pp, szp, ci, intp]
+    L.rsgpu_encode_verify.argtypes = [vp, u8pp, szp, ci, intp]
     L.rsgpu_reconstruct.argtypes = [vp, u8pp, szp, ci, ci]
     L.rsgpu_decode.argtypes = [vp, u8pp, szp, ci, intp]
     L.rsgpu_update.argtypes = [vp, u8pp, szp, ci, u8pp, szp, ci]

@@ -153,10 +153,15 @@ class Client:
 
     # -------------------------------------------------------------- codec
     def encode(self, obj) -> List:
-        """ecRedis.go:382-402: Split -> Encode -> Verify."""
+        """ecRedis.go:382-402: Split -> Encode -> Verify (with ``fused_decode``
+        and a GPU codec, the Encode+Verify pair is one device round trip,
+        RSEncoder.EncodeVerify)."""
         shards = self.EC.Split(obj)
-        self.EC.Encode(shards)
-        ok = self.EC.Verify(shards)
+        if self.fused_decode and hasattr(self.EC, "EncodeVerify"):
+            ok = self.EC.EncodeVerify(shards)
+        else:
+            self.EC.Encode(shards)
+            ok = self.EC.Verify(shards)
         if not ok:
             raise RSError("Failed to verify encoding")
         return shards

@@ -135,9 +135,12 @@ namespace {
 //     layout) and go as one DMA;
 //   * written rows come back the same way (pinned: straight into the caller's
 //     buffers).
+//   * `then` (optional): a second plan run on the same device image after the
+//     first one's rows went back, whose check flag lands in *then_bad
+//     (Client.encode's Verify right after Encode: no second upload).
 int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
              const std::vector<const uint8_t *> &in_src, const std::vector<uint8_t *> &out_dst,
-             uint32_t *bad) {
+             uint32_t *bad, Plan *then = nullptr, uint32_t *then_bad = nullptr) {
     // row offsets are 32-bit inside the pass (Pass::in_off / out_off)
     if ((size_t)nrows_staged * size + 16 >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
     std::unique_ptr<Slot> s;
@@ -194,6 +197,11 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     }
     if (he == hipSuccess && plan.nw < plan.R)
         he = hipMemcpyAsync(s->h_bad, s->d_bad, 4, hipMemcpyDeviceToHost, s->stream);
+    if (then && he == hipSuccess) {  // check-only plan (nw == 0) on the image as it stands
+        if (he == hipSuccess) he = hipMemsetAsync(s->d_bad, 0, 4, s->stream);
+        if (he == hipSuccess) he = launch_plan(*then, Layout{s->d, 0, size, size, 1}, s->d_bad, s->stream);
+        if (he == hipSuccess) he = hipMemcpyAsync(s->h_bad, s->d_bad, 4, hipMemcpyDeviceToHost, s->stream);
+    }
     if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
     if (he != hipSuccess) {
         (void)hipStreamSynchronize(s->stream);  // nothing in flight may touch a pooled slot
@@ -203,6 +211,7 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     if (!pin_out)
         for (int r = 0; r < plan.nw; ++r) std::memcpy(out_dst[r], s->h + (size_t)orows[r] * size, size);
     if (bad) *bad = plan.nw < plan.R ? *s->h_bad : 0;
+    if (then_bad) *then_bad = *s->h_bad;
     ctx->put_slot(std::move(s));
     return RSGPU_OK;
 }
@@ -305,6 +314,25 @@ int rsgpu_encode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
     std::vector<const uint8_t *> in(shards, shards + ctx->k);
     std::vector<uint8_t *> out(shards + ctx->k, shards + ctx->n);
     return run_host(ctx, *plan, ctx->n, size, in, out, nullptr);
+}
+
+int rsgpu_encode_verify(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
+    if (!ctx || !shards || !lens || !ok) return RSGPU_ERR_INVALID_ARG;
+    *ok = 0;
+    if (nshards != ctx->n) return RSGPU_ERR_TOO_FEW_SHARDS;
+    size_t size;
+    int e = check_shards(lens, nshards, false, &size);
+    if (e) return e;
+    if ((e = ctx->use_device())) return e;
+    auto enc = ctx->plan_encode();
+    auto ver = ctx->plan_verify();
+    std::vector<const uint8_t *> in(shards, shards + ctx->k);
+    std::vector<uint8_t *> out(shards + ctx->k, shards + ctx->n);
+    uint32_t bad = 1;
+    e = run_host(ctx, *enc, ctx->n, size, in, out, nullptr, ver.get(), &bad);
+    if (e) return e;
+    *ok = bad == 0;
+    return RSGPU_OK;
 }
 
 int rsgpu_verify(rsgpu_ctx *ctx, const uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {

@@ -225,6 +225,15 @@ class RSEncoder:
         _check(self._L.rsgpu_verify(self._ctx, t.ptrs, t.lens, len(shards), ctypes.byref(ok)))
         return bool(ok.value)
 
+    def EncodeVerify(self, shards: Sequence) -> bool:
+        """Client.encode's Encode then Verify (ecRedis.go:390-395) in one
+        device round trip: parity written into shards[k:], then every parity
+        shard re-checked on the device image; returns Verify's boolean."""
+        t = _ShardTable(shards, writable_idx=range(self.DataShards, len(shards)))
+        ok = ctypes.c_int(0)
+        _check(self._L.rsgpu_encode_verify(self._ctx, t.ptrs, t.lens, len(shards), ctypes.byref(ok)))
+        return bool(ok.value)
+
     def _prepare_missing(self, shards: list, data_only: bool):
         """upstream reconstruct(): missing shards get a buffer of the shard
         size (re-using capacity is a Go notion; Python allocates)."""

@@ -112,6 +112,11 @@ static int gpu_checks(void) {
     CHECK(rsgpu_encode(ctx, ps, lens, n) == RSGPU_OK);
     for (int i = k; i < n; i++) CHECK(memcmp(ps[i], ref[i], S) == 0);
     CHECK(rsgpu_verify(ctx, (const uint8_t *const *)ps, lens, n, &ok) == RSGPU_OK && ok == 1);
+    /* Client.encode fused: Encode then Verify in one device round trip */
+    for (int i = k; i < n; i++) memset(ps[i], 0x11, S);
+    ok = 0;
+    CHECK(rsgpu_encode_verify(ctx, ps, lens, n, &ok) == RSGPU_OK && ok == 1);
+    for (int i = k; i < n; i++) CHECK(memcmp(ps[i], ref[i], S) == 0);
     int plost[4] = {2, 3, 9, 12};
     for (int j = 0; j < 4; j++) { memset(ps[plost[j]], 0x77, S); lens[plost[j]] = 0; }
     CHECK(rsgpu_reconstruct(ctx, ps, lens, n, 0) == RSGPU_OK);

@@ -82,6 +82,13 @@ def test_error_precedence_without_device():
         enc.Encode([None] * 6)
     with pytest.raises(ia.ErrShardSize):
         enc.Verify([bytearray(8)] * 5 + [bytearray(7)])
+    # fused Client.encode (Encode then Verify): Encode's checks, same order
+    with pytest.raises(ia.ErrTooFewShards):
+        enc.EncodeVerify([bytearray(8)] * 5)
+    with pytest.raises(ia.ErrShardSize):
+        enc.EncodeVerify([bytearray(8)] * 5 + [None])
+    with pytest.raises(ia.ErrShardNoData):
+        enc.EncodeVerify([None] * 6)
     with pytest.raises(ia.ErrTooFewShards):
         enc.Reconstruct([bytearray(8)] * 3 + [None] * 3)
     with pytest.raises(ia.ErrTooFewShards):
@@ -101,6 +108,8 @@ def test_compute_fails_loudly_without_device():
         enc.Encode([bytearray(8)] * 6)
     with pytest.raises(ia.NoDevice):
         enc.Verify([bytearray(8)] * 6)
+    with pytest.raises(ia.NoDevice):
+        enc.EncodeVerify([bytearray(8)] * 6)
     with pytest.raises(ia.NoDevice):
         enc.Reconstruct([None] + [bytearray(8)] * 5)
     with pytest.raises(ia.NoDevice):

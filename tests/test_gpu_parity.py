@@ -84,6 +84,28 @@ def test_encode_verify_sizes(gpu, size):
         assert not enc.Verify(bad)
 
 
+@pytest.mark.parametrize("k,p,size", [(10, 2, 104858), (10, 4, 4097), (10, 2, 1), (3, 13, 77),
+                                      (20, 4, 1000)])
+def test_encode_verify_fused(gpu, k, p, size):
+    """Client.encode's Encode+Verify in one device round trip: parity equal to
+    the oracle's, ok, from pageable and pinned (Split-layout) buffers."""
+    want = _full(k, p, size, idx=7 * size + k)
+    enc = ia.New(k, p)
+    sh = [want[i].copy() for i in range(k)] + [np.full(size, 0x3C, np.uint8) for _ in range(p)]
+    assert enc.EncodeVerify(sh)
+    for r in range(k, k + p):
+        assert np.array_equal(sh[r], want[r])
+    host = ia.host_alloc((k + p) * size)
+    ps = [host[i * size:(i + 1) * size] for i in range(k + p)]
+    for i in range(k):
+        ps[i][:] = want[i]
+    for r in range(k, k + p):
+        ps[r][:] = 0
+    assert enc.EncodeVerify(ps)
+    for r in range(k, k + p):
+        assert np.array_equal(ps[r], want[r])
+
+
 def test_encode_zero_and_ff(gpu):
     """log(0) edge: all-zero and all-0xFF objects."""
     enc = ia.New(10, 2)

@@ -1,6 +1,7 @@
 /* lat_bench.c — per-object latency of the host-buffer C ABI, as the cgo shim
  *  drives it for one EcSet / EcGet: Client.encode = Encode +
- * Verify, Client.decode = Reconstruct + Verify (fused, rsgpu_decode), 1 MiB
+ * Verify (separate calls, and fused: rsgpu_encode_verify), Client.decode =
+ * Reconstruct + Verify (fused, rsgpu_decode), 1 MiB
  * RS(10+2) objects, shards as Split lays them out (one contiguous buffer).
  *
  *   ./lat_bench [iters]
@@ -40,6 +41,7 @@ int main(int argc, char **argv) {
     rsgpu_ctx *ctx;
     if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
     double *te = malloc(sizeof(double) * iters), *td = malloc(sizeof(double) * iters);
+    double *tf = malloc(sizeof(double) * iters);
     for (int pinned = 0; pinned < 2; ++pinned) {
         uint8_t *buf = NULL, *keep = malloc(S);
         if (pinned) {
@@ -68,11 +70,17 @@ int main(int argc, char **argv) {
             if (rsgpu_decode(ctx, sh, lens, n, &ok) || !ok) return 4;
             double t3 = now_us();
             if (memcmp(keep, sh[0], S)) { fprintf(stderr, "decode mismatch\n"); return 5; }
-            if (it >= warm) { te[it - warm] = t1 - t0; td[it - warm] = t3 - t2; }
+            lens[0] = lens[5] = S;
+            double t4 = now_us();  /* the same pair fused (rsgpu_encode_verify) */
+            if (rsgpu_encode_verify(ctx, sh, lens, n, &ok) || !ok) return 6;
+            double t5 = now_us();
+            if (it >= warm) { te[it - warm] = t1 - t0; td[it - warm] = t3 - t2; tf[it - warm] = t5 - t4; }
         }
         printf("%-8s encode+verify p50 %7.1f us  p99 %7.1f us   decode p50 %7.1f us  p99 %7.1f us\n",
                pinned ? "pinned" : "pageable", pct(te, iters, 0.5), pct(te, iters, 0.99), pct(td, iters, 0.5),
                pct(td, iters, 0.99));
+        printf("%-8s encode+verify fused (rsgpu_encode_verify) p50 %7.1f us  p99 %7.1f us\n",
+               pinned ? "pinned" : "pageable", pct(tf, iters, 0.5), pct(tf, iters, 0.99));
         if (pinned) rsgpu_host_free(buf); else free(buf);
         free(keep);
     }
