@@ -54,6 +54,15 @@ constexpr int kMultiChunks = 1; // chunks per workgroup in the mixed-pattern ker
 // launches whose objects span more than this use the XCD-contiguous workgroup
 // order (gf_device.h Order); 0: every launch
 constexpr size_t kXcdSpan = 0;
+// Occupancy cap for passes that store rows: a dynamic LDS reservation (the
+// kernels use no LDS) of 1/4 of the CU's 160 KiB leaves room for 4
+// workgroups = 16 waves per CU instead of 8 x 4.  Fewer concurrent row
+// streams keep DRAM pages open longer: +1-2 points of HBM peak on every
+// writing plan, cold (encode RS(10+2) 74.2 vs 72.5 %, fused decode 73.2 vs
+// 71.5 %, ReconstructData RS(10+4) 74.4 vs 73.3 %; r01_kbench_cold_occ_*).
+// Check-only passes (Verify) keep full occupancy: the VALU-bound RS(10+4)
+// verify drops from 81.5 to 76.1 % under the cap.
+constexpr unsigned kStoreLds = 160u * 1024u / 4u - 256u;
 constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
 constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
@@ -215,7 +224,7 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
         hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
-                           dim3(kBlock), 0, st, a);
+                           dim3(kBlock), a.p.nw ? kStoreLds : 0u, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -279,6 +288,8 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
         objs[j] = items[j].first;
         pidx[j] = items[j].second;
     }
+    bool stores = false;
+    for (const Entry *e : es) stores |= e->sub.nw > 0;
     return [=](const uint8_t *dimg, hipStream_t st) -> hipError_t {
         MultiArgs<K, R> m;
         m.base = L.base;
@@ -297,7 +308,7 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
             unsigned grid;
             m.ord = make_order(gx, (uint32_t)no, objs_span(L, no, L.pitch * 256), grid);
             hipLaunchKernelGGL((gf_apply_multi<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kMultiChunks>),
-                               dim3(grid), dim3(kBlock), 0, st, m);
+                               dim3(grid), dim3(kBlock), stores ? kStoreLds : 0u, st, m);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -374,7 +385,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
-        hipLaunchKernelGGL((gf_apply_generic<R>), dim3(grid), dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL((gf_apply_generic<R>), dim3(grid), dim3(kBlock), a.nw ? kStoreLds : 0u, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -158,6 +158,16 @@ void launch_v(const void *args, dim3 grid, hipStream_t st) {
     a.ord = order_for<ORD>(grid, (size_t)grid.y * a.obj_stride, nb);
     hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA>), dim3(nb), dim3(BS), 0, st, a);
 }
+// the library's launch exactly: nt loads/stores, XCD-contiguous order, and
+// the 4-workgroups-per-CU LDS occupancy cap on passes that store rows
+template <int K, int R>
+void launch_ship(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, 2, 2>), dim3(nb), dim3(256),
+                       a.p.nw ? 160u * 1024u / 4u - 256u : 0u, st, a);
+}
 template <int K, int R>
 void launch_x(const void *args, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((xor_only<K, R>), grid, dim3(256), 0, st, *(const ApplyArgs<K, R> *)args);
@@ -307,11 +317,67 @@ void launch_rg(const void *args, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((apply_regions<K, R, M, BS, 2, 2>), dim3(per * 8 * M), dim3(BS), 0, st, a, per);
 }
 
+// occupancy cap: a dynamic LDS reservation of 160 KiB / W per workgroup
+// leaves room for at most W workgroups (4 waves each) per CU
+template <int K, int R, int W, int U = 1, int BS = 256>
+void launch_occ(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, 2, 2>), dim3(nb), dim3(BS), (160 * 1024) / W - 256, st, a);
+}
+
+// persistent form: W workgroups per CU (256 CUs), each walking the items of
+// its XCD's contiguous share with stride = workgroups per XCD
+template <int K, int R>
+__global__ __launch_bounds__(256) void apply_persist(const ApplyArgs<K, R> a, uint32_t per_xcd) {
+    const uint32_t b = blockIdx.x, x = b & 7u, t = b >> 3, T = gridDim.x >> 3;
+    const uint32_t xper = (a.ord.total + 7) / 8;
+    (void)per_xcd;
+    for (uint32_t i = t; i < xper; i += T) {
+        const uint32_t w = x * xper + i;
+        if (w >= a.ord.total) break;
+        const uint32_t obj = w / a.ord.nchunk, chunk = w - obj * a.ord.nchunk;
+        gf_apply_body<K, R, 1, 256, 2, 2>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec, a.tail,
+                                          a.bad, chunk * 256 + threadIdx.x);
+    }
+}
+template <int K, int R, int W>
+void launch_pers(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    a.ord.nchunk = grid.x;
+    a.ord.total = grid.x * grid.y;
+    hipLaunchKernelGGL((apply_persist<K, R>), dim3(256 * W), dim3(256), 0, st, a, 0u);
+}
+
+// KB_SET=occ: occupancy sweep
+template <int K, int R>
+std::vector<Variant> occ_variants() {
+    return {
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"nt/nt, full occupancy", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"occ<=1 U1", launch_occ<K, R, 1>, 1, 256, false},
+        {"occ<=2 U1", launch_occ<K, R, 2>, 1, 256, false},
+        {"occ<=3 U1", launch_occ<K, R, 3>, 1, 256, false},
+        {"occ<=4 U1", launch_occ<K, R, 4>, 1, 256, false},
+        {"occ<=5 U1", launch_occ<K, R, 5>, 1, 256, false},
+        {"occ<=1 U2", launch_occ<K, R, 1, 2>, 2, 256, false},
+        {"occ<=2 U2", launch_occ<K, R, 2, 2>, 2, 256, false},
+        {"occ<=1 B512", launch_occ<K, R, 1, 1, 512>, 1, 512, false},
+        {"occ<=2 B512", launch_occ<K, R, 2, 1, 512>, 1, 512, false},
+        {"occ<=1 B1024", launch_occ<K, R, 1, 1, 1024>, 1, 1024, false},
+        {"persistent W=2", launch_pers<K, R, 2>, 1, 256, false},
+        {"persistent W=4", launch_pers<K, R, 4>, 1, 256, false},
+        {"persistent W=8", launch_pers<K, R, 8>, 1, 256, false},
+    };
+}
+
 // KB_SET=order: cold-HBM sweep of the launch order with nt/nt policy
 template <int K, int R>
 std::vector<Variant> order_variants() {
     return {
-        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"nt/nt, full occupancy", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
         {"nt/sc1 (pre-retune)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
         {"nt/nt linear", launch_v<K, R, 1, 256, 2, 2, false, 1>, 1, 256, false},
         {"nt/nt XCD-contiguous", launch_v<K, R, 1, 256, 2, 2, false, 2>, 1, 256, false},
@@ -323,6 +389,10 @@ std::vector<Variant> order_variants() {
         {"B128 nt/nt regions M=1", launch_rg<K, R, 1, 128>, 1, 128, false},
         {"B128 nt/nt regions M=2", launch_rg<K, R, 2, 128>, 1, 128, false},
         {"B512 nt/nt regions M=1", launch_rg<K, R, 1, 512>, 1, 512, false},
+        {"occupancy <= 2 WG/CU", launch_occ<K, R, 2>, 1, 256, false},
+        {"occupancy <= 3 WG/CU", launch_occ<K, R, 3>, 1, 256, false},
+        {"occupancy <= 4 WG/CU", launch_occ<K, R, 4>, 1, 256, false},
+        {"occupancy <= 6 WG/CU", launch_occ<K, R, 6>, 1, 256, false},
         {"xor-only, SA nt", launch_xs<K, R, 2>, 1, 256, true},
     };
 }
@@ -332,7 +402,8 @@ std::vector<Variant> order_variants() {
 template <int K, int R>
 std::vector<Variant> policy_variants() {
     return {
-        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"nt/nt, full occupancy", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
         {"LA nt / SA sc1 (pre-retune)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
         {"LA nt / SA 0", launch_v<K, R, 1, 256, 2, 0>, 1, 256, false},
         {"LA nt / SA sc0", launch_v<K, R, 1, 256, 2, 1>, 1, 256, false},
@@ -435,7 +506,8 @@ void launch_2p(const void *args, dim3 grid, hipStream_t st) {
 template <int K, int R>
 std::vector<Variant> twophase_variants() {
     return {
-        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"nt/nt, full occupancy", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
         {"2-phase SB=64 sc1", launch_2p<K, R, 64, 16, 16>, 1, 256, false},
         {"2-phase SB=128 sc1", launch_2p<K, R, 128, 16, 16>, 1, 256, false},
         {"2-phase SB=256 sc1", launch_2p<K, R, 256, 16, 16>, 1, 256, false},
@@ -450,7 +522,8 @@ std::vector<Variant> twophase_variants() {
 template <int K, int R>
 std::vector<Variant> stream_variants() {
     return {
-        {"shipped (nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"nt/nt, full occupancy", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
         {"read-only, K rows", launch_sr<K, R>, 1, 256, true, K, 0},
         {"write-only, 2 rows", launch_sw<K, R, 2>, 1, 256, true, 0, 2},
         {"write-only, 12 rows", launch_sw<K, R, 12>, 1, 256, true, 0, 12},
@@ -461,11 +534,13 @@ std::vector<Variant> stream_variants() {
 template <int K, int R>
 std::vector<Variant> variants() {
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "stream") return stream_variants<K, R>();
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "occ") return occ_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "twophase") return twophase_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "policy") return policy_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "order") return order_variants<K, R>();
     return {
-        {"shipped(U1,B256,nt/nt)", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"nt/nt, full occupancy", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
         {"nt/sc1 (pre-retune)", launch_v<K, R, 1, 256, 2, 16>, 1, 256, false},
         {"no identity inputs", launch_v<K, R, 1, 256, 2, 2, true>, 1, 256, false},
         {"nt/sc01", launch_v<K, R, 1, 256, 2, 17>, 1, 256, false},
