@@ -350,6 +350,35 @@ void launch_pers(const void *args, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((apply_persist<K, R>), dim3(256 * W), dim3(256), 0, st, a, 0u);
 }
 
+// KB_SET=rows: the same pass on another row assignment (timing only): inputs
+// on rows 0..K-1 and outputs on K..K+R-1 (encode's layout), or inputs on
+// {1-4, 6-11} and outputs on {0, 5} (the healthy-Get decode's layout)
+template <int K, int R, int LAYOUT>
+void launch_rows(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    if (LAYOUT == 0) {
+        for (int c = 0; c < K; ++c) a.p.in_off[c] = c * g_pitch;
+        for (int r = 0; r < R; ++r) a.p.out_off[r] = (K + r) * g_pitch;
+    } else {
+        static const int in[12] = {1, 2, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13};
+        static const int out[4] = {0, 5, 12, 13};
+        for (int c = 0; c < K; ++c) a.p.in_off[c] = in[c] * g_pitch;
+        for (int r = 0; r < R; ++r) a.p.out_off[r] = out[r] * g_pitch;
+    }
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, 2, 2>), dim3(nb), dim3(256),
+                       a.p.nw ? 160u * 1024u / 4u - 256u : 0u, st, a);
+}
+template <int K, int R>
+std::vector<Variant> rows_variants() {
+    return {
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"encode's row layout", launch_rows<K, R, 0>, 1, 256, true},
+        {"decode's row layout", launch_rows<K, R, 1>, 1, 256, true},
+    };
+}
+
 // KB_SET=occ: occupancy sweep
 template <int K, int R>
 std::vector<Variant> occ_variants() {
@@ -534,6 +563,7 @@ std::vector<Variant> stream_variants() {
 template <int K, int R>
 std::vector<Variant> variants() {
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "stream") return stream_variants<K, R>();
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "rows") return rows_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "occ") return occ_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "twophase") return twophase_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "policy") return policy_variants<K, R>();
@@ -781,7 +811,9 @@ int setup_bufs(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, const std::vector
 
 template <int K, int R>
 int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
-    const std::vector<size_t> pads = {0, 256, 512, 1024, 2048, 4096, 4096 + 256, 65536 + 256};
+    // every buffer is revisited only after the other pads' buffers (>= 9 GB of
+    // traffic), so this sweep is cold
+    const std::vector<size_t> pads = {0, 128, 256, 512, 768, 1024, 1536, 2048, 3072, 4096, 8192};
     const int np = (int)pads.size();
     std::vector<uint8_t *> bufs;
     std::vector<ApplyArgs<K, R>> args;
@@ -798,7 +830,7 @@ int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, cons
     for (int it = 0; it < rounds + 3; ++it)
         for (int i = 0; i < np; ++i) {
             CK(hipEventRecord(e0, st));
-            launch_v<K, R, 1, 256, 2, 2>(&args[i], grid, st);
+            launch_ship<K, R>(&args[i], grid, st);
             CK(hipEventRecord(e1, st));
             CK(hipEventSynchronize(e1));
             float t;
