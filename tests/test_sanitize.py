@@ -1,0 +1,63 @@
+"""Host-side AddressSanitizer + UndefinedBehaviorSanitizer over the C ABI
+(no sanitizers in the reference; the build runs its host code
+under ASan/UBSan).  `make -C infinicache_amd/csrc sanitize` instruments the
+host compile of rsgpu.cpp / pipeline.cpp (argument checks, plan and inverse
+caches, staging slots, pipelines); device code is never instrumented (the
+-fsanitize flags go to -Xarch_host only).  tests/c_abi_client.c and the CPU
+oracle (its checker) are built with the same clang and the same runtimes.
+Any ASan/UBSan report aborts the client (halt_on_error)."""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SAN = os.path.join(ROOT, "tools", "san")
+CLANG = "/opt/rocm/lib/llvm/bin/clang"
+
+
+def _runtime_dir():
+    r = subprocess.run([CLANG, "-print-resource-dir"], capture_output=True, text=True, check=True)
+    return os.path.join(r.stdout.strip(), "lib", "linux")
+
+
+@pytest.fixture(scope="module")
+def san_client():
+    if not os.path.exists(CLANG):
+        pytest.skip("no clang in this image")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "infinicache_amd", "csrc"), "sanitize"])
+    out = os.path.join(SAN, "c_abi_client_san")
+    rt = _runtime_dir()
+    subprocess.check_call([
+        CLANG, "-O1", "-g", "-std=c11", "-D_GNU_SOURCE", "-fsanitize=address,undefined",
+        "-shared-libasan", "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "include"),
+        "-I", os.path.join(ROOT, "oracle"), os.path.join(HERE, "c_abi_client.c"),
+        os.path.join(ROOT, "oracle", "rs_oracle.c"), "-o", out, "-L", SAN, "-l:librsgpu_san.so",
+        "-Wl,-rpath," + SAN, "-Wl,-rpath," + rt, "-lpthread"])
+    return out
+
+
+def _run(binary, *args, timeout=300):
+    env = dict(os.environ)
+    # the HIP runtime keeps process-lifetime allocations: leak checking off
+    env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1"
+    env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
+    return subprocess.run([binary, *args], capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def test_c_abi_host_paths_under_asan_ubsan(san_client):
+    r = _run(san_client)
+    assert r.returncode == 0, r.stderr[-4000:] + r.stdout
+    assert "host checks ok" in r.stdout
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+@pytest.mark.gpu
+def test_c_abi_gpu_paths_under_asan_ubsan(gpu, san_client):
+    """The host side of every GPU path (staging, pinned DMA, pipelines,
+    mixed-pattern images) under ASan/UBSan, with the kernels running."""
+    r = _run(san_client, "gpu")
+    assert r.returncode == 0, r.stderr[-4000:] + r.stdout
+    assert "gpu checks ok" in r.stdout
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
