@@ -555,15 +555,25 @@ def main():
     e_rows = len(w["lost"])
     enc_bytes = nobj * (k + p) * S
     dec_bytes = nobj * (k + e_rows) * S
-    per_kernel = {}
+    # launches grouped by kernel symbol: encode and the uniform-pattern decode
+    # of RS(10+2) are the same kernel (gf_apply_kernel<10,2>) with the same
+    # algorithmic bytes per launch, so its average duration is over both, as
+    # rocprofv3 --stats reports it
+    enc_sym = f"gf_apply_kernel<{k},{p}>"
+    dec_sym = f"gf_apply_{'multi' if w.get('mixed') else 'kernel'}<{k},{e_rows}>"
+    per_op = {}
     if "encode" in w["ops"]:
-        per_kernel["encode"] = (enc_bytes, enc_ms)
+        per_op["encode"] = (enc_sym, enc_bytes, enc_ms)
     if "decode" in w["ops"]:
-        per_kernel["decode"] = (dec_bytes, dec_ms)
-    dom = max(per_kernel, key=lambda x: per_kernel[x][1])
-    dom_bytes, dom_ms = per_kernel[dom]
+        per_op["decode"] = (dec_sym, dec_bytes, dec_ms)
+    groups = {}
+    for op, (sym, b, ms) in per_op.items():
+        groups.setdefault((sym, b), []).append((op, ms))
+    # dominant: the kernel with the most time per step
+    (kernel_key, dom_bytes), members = max(groups.items(), key=lambda kv: sum(m for _, m in kv[1]))
+    dom_ms = float(np.mean([m for _, m in members]))
+    dom = "+".join(op for op, _ in members)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    kernel_key = f"gf_apply_kernel<{k},{p if dom == 'encode' else e_rows}>"
     traffic = pmc_traffic(kernel_key, args.workload, dom_bytes)
     roofline = {
         "bound": "hbm",
@@ -572,16 +582,17 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "kernel": f"{kernel_key} ({dom}), {dom_bytes} algorithmic B/launch, "
+        "kernel": f"{kernel_key} ({dom} launches), {dom_bytes} algorithmic B/launch, "
                   f"{dom_ms * 1e3:.1f} us avg (HIP events on {len(evs)} of {args.steps} timed steps)",
-        "per_kernel_GBps": {kk: round(b / (ms * 1e-3) / 1e9, 1) for kk, (b, ms) in per_kernel.items()},
+        "per_kernel_GBps": {op: round(b / (ms * 1e-3) / 1e9, 1) for op, (_, b, ms) in per_op.items()},
     }
 
     warm = None
     if args.warm:
         warm = {
             "value": round(objs_all * w["nbytes"] * ops * args.steps / warm_el / GiB, 2),
-            "frac": round(dom_bytes / (warm_ms[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac": round(dom_bytes / (float(np.mean([warm_ms[op] for op, _ in members])) * 1e-3)
+                          / 1e9 / HBM_PEAK_GBS, 4),
             "note": "one batch re-coded every step: its parity rewrites hit the 256 MiB Infinity "
                     "Cache, so this is not an HBM rate (reported for comparison, not the value)",
         }
