@@ -54,15 +54,22 @@ constexpr int kMultiChunks = 1; // chunks per workgroup in the mixed-pattern ker
 // launches whose objects span more than this use the XCD-contiguous workgroup
 // order (gf_device.h Order); 0: every launch
 constexpr size_t kXcdSpan = 0;
-// Occupancy cap for passes that store rows: a dynamic LDS reservation (the
-// kernels use no LDS) of 1/4 of the CU's 160 KiB leaves room for 4
-// workgroups = 16 waves per CU instead of 8 x 4.  Fewer concurrent row
-// streams keep DRAM pages open longer: +1-2 points of HBM peak on every
-// writing plan, cold (encode RS(10+2) 74.2 vs 72.5 %, fused decode 73.2 vs
-// 71.5 %, ReconstructData RS(10+4) 74.4 vs 73.3 %; r01_kbench_cold_occ_*).
+// Occupancy cap for passes that store rows.  The kernels use no LDS, so a
+// dynamic LDS reservation of 1/W of the CU's 160 KiB caps residency at W
+// workgroups (4 waves each) per CU.  Fewer concurrent row streams keep DRAM
+// pages open longer; the best W keeps about 160 KiB of input loads in flight
+// per CU (K rows x 4 KiB per workgroup): W = 40 / K, clamped to [2, 8]
+// (tools/kbench KB_SET=occ, cold, r01_kbench_cold_occ_*):
+//   encode RS(8+4)   W=4: 75.9 vs 73.2 % full occupancy
+//   encode RS(10+2)  W=4: 74.0 vs 72.5 %; ReconstructData RS(10+4) 75.0 vs 73.9 %
+//   encode RS(12+4)  W=3: 73.4 vs 68.5 % (W=2: 74.1)
+//   encode RS(16+4)  W=2: 77.8 vs 73.7 %;  encode RS(16+2) W=2: 80.1 vs 76.4 %
 // Check-only passes (Verify) keep full occupancy: the VALU-bound RS(10+4)
-// verify drops from 81.5 to 76.1 % under the cap.
-constexpr unsigned kStoreLds = 160u * 1024u / 4u - 256u;
+// verify drops from 84.3 to 77.7 % under a cap of 4.
+constexpr unsigned store_lds(int K) {
+    const int w = K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K);
+    return 160u * 1024u / (unsigned)w - 256u;
+}
 constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
 constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
@@ -104,8 +111,13 @@ Plan::~Plan() {
     if (d_in_row) (void)hipFree(d_in_row);
 }
 
-// Generic pass for K > 16 inputs (any shard count up to 256): runtime input
-// loop, tables read by scalar loads from a device buffer [K][R][kTabWords].
+// Generic pass for K > 16 inputs (any shard count up to 256) and up to
+// kMaxRG = 8 rows per pass: runtime input loop over groups of G inputs whose
+// G loads are issued together (memory-level parallelism inside the wave),
+// tables and row indices read with scalar loads from a device image
+// [K][rstride][kTabWords] (constant address space: s_load).
+constexpr int kMaxRG = 8;
+constexpr int kGroup = 4;
 struct GenericArgs {
     const uint8_t *base;
     uint64_t obj_stride;
@@ -114,10 +126,10 @@ struct GenericArgs {
     const uint32_t *in_row;  // [K] row indices; offset = row * pitch
     uint32_t nvec, tail, nw, span, K, rstride, pitch, clear, packed;
     Order ord;  // item = object
-    uint32_t out_off[kMaxR];
+    uint32_t out_off[kMaxRG];
 };
 
-template <int R>
+template <int R, int G>
 __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
@@ -127,21 +139,37 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
     const uint32_t voff = v * 16u;
+    const constant_ptr<uint32_t> tab = (constant_ptr<uint32_t>)a.tab;
+    const constant_ptr<uint32_t> rows = (constant_ptr<uint32_t>)a.in_row;
     uint32_t acc[R][4];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int d = 0; d < 4; ++d) acc[r][d] = 0;
-    for (uint32_t c = 0; c < a.K; ++c) {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_row[c] * a.pitch, kLoadAux);
-        const uint32_t *t = a.tab + (size_t)c * a.rstride * kTabWords;
+    auto mac_input = [&](const u32x4 &x, uint32_t c) {
+        const constant_ptr<uint32_t> t = tab + (size_t)c * a.rstride * kTabWords;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
             const GfIdx g = gf_idx(x[d]);
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], t + r * kTabWords, g);
         }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+    };
+    uint32_t c = 0;
+    for (; c + G <= a.K; c += G) {
+        u32x4 x[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            x[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c + g] * a.pitch, kLoadAux);
+#pragma unroll
+        for (int g = 0; g < G; ++g) mac_input(x[g], c + g);
     }
+    for (; c < a.K; ++c)
+        mac_input(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux), c);
     bool mismatch = false;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -224,7 +252,7 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
         hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
-                           dim3(kBlock), a.p.nw ? kStoreLds : 0u, st, a);
+                           dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -308,7 +336,7 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
             unsigned grid;
             m.ord = make_order(gx, (uint32_t)no, objs_span(L, no, L.pitch * 256), grid);
             hipLaunchKernelGGL((gf_apply_multi<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kMultiChunks>),
-                               dim3(grid), dim3(kBlock), stores ? kStoreLds : 0u, st, m);
+                               dim3(grid), dim3(kBlock), stores ? store_lds(K) : 0u, st, m);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -385,7 +413,9 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
-        hipLaunchKernelGGL((gf_apply_generic<R>), dim3(grid), dim3(kBlock), a.nw ? kStoreLds : 0u, st, a);
+        // full occupancy: the wide generic passes are VALU-bound (tools/kbench
+        // lib:SHAPE with caps of 2/4/6 workgroups per CU: -8/-1/+0.8 points)
+        hipLaunchKernelGGL((gf_apply_generic<R, kGroup>), dim3(grid), dim3(kBlock), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -427,16 +457,20 @@ hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
         }
         return hipSuccess;
     }
-    // K > 16: generic kernel, one pass per <= 4 rows over one table image
-    for (int r0 = 0; r0 < p.R; r0 += kMaxR) {
-        Sub s{r0, std::min(kMaxR, p.R - r0), 0};
+    // K > 16: generic kernel, one pass per <= 8 rows over one table image
+    for (int r0 = 0; r0 < p.R; r0 += kMaxRG) {
+        Sub s{r0, std::min(kMaxRG, p.R - r0), 0};
         s.nw = std::max(0, std::min(s.R, p.nw - r0));
         hipError_t e;
         switch (s.R) {
             case 1: e = launch_generic<1>(p, s, L, d_bad, st); break;
             case 2: e = launch_generic<2>(p, s, L, d_bad, st); break;
             case 3: e = launch_generic<3>(p, s, L, d_bad, st); break;
-            default: e = launch_generic<4>(p, s, L, d_bad, st); break;
+            case 4: e = launch_generic<4>(p, s, L, d_bad, st); break;
+            case 5: e = launch_generic<5>(p, s, L, d_bad, st); break;
+            case 6: e = launch_generic<6>(p, s, L, d_bad, st); break;
+            case 7: e = launch_generic<7>(p, s, L, d_bad, st); break;
+            default: e = launch_generic<8>(p, s, L, d_bad, st); break;
         }
         if (e != hipSuccess) return e;
     }

@@ -165,8 +165,9 @@ void launch_ship(const void *args, dim3 grid, hipStream_t st) {
     ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
     unsigned nb;
     a.ord = order_for<0>(grid, 0, nb);
+    const int w = K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K);  // gf_kernels.hip store_lds
     hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, 2, 2>), dim3(nb), dim3(256),
-                       a.p.nw ? 160u * 1024u / 4u - 256u : 0u, st, a);
+                       a.p.nw ? 160u * 1024u / (unsigned)w - 256u : 0u, st, a);
 }
 template <int K, int R>
 void launch_x(const void *args, dim3 grid, hipStream_t st) {
@@ -258,6 +259,14 @@ __global__ __launch_bounds__(256) void stream_write(const ApplyArgs<K, R> a, uin
     for (int r = 0; r < W; ++r) __builtin_amdgcn_raw_buffer_store_b128(o, rs, v * 16u, r * pitch, 2);
 }
 static uint32_t g_pitch = 0;
+// the library's own launch_plan on the same buffers (sanity: must equal "shipped")
+static Plan *g_plan = nullptr;
+static size_t g_S = 0;
+template <int K, int R>
+void launch_lib(const void *args, dim3 grid, hipStream_t st) {
+    const ApplyArgs<K, R> &a = *(const ApplyArgs<K, R> *)args;
+    (void)launch_plan(*g_plan, Layout{(uint8_t *)a.base, a.obj_stride, g_pitch, g_S, (int)grid.y}, a.bad, st);
+}
 template <int K, int R>
 void launch_sr(const void *args, dim3 grid, hipStream_t st) {
     ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
@@ -385,6 +394,7 @@ std::vector<Variant> occ_variants() {
     return {
         {"shipped", launch_ship<K, R>, 1, 256, false},
         {"nt/nt, full occupancy", launch_v<K, R, 1, 256, 2, 2>, 1, 256, false},
+        {"library launch_plan", launch_lib<K, R>, 1, 256, false},
         {"occ<=1 U1", launch_occ<K, R, 1>, 1, 256, false},
         {"occ<=2 U1", launch_occ<K, R, 2>, 1, 256, false},
         {"occ<=3 U1", launch_occ<K, R, 3>, 1, 256, false},
@@ -608,6 +618,8 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
     // one batch, which a 1.3 GB sweep partly re-reads from that cache)
     const int NB = std::max(1, std::getenv("KB_ROT") ? std::atoi(std::getenv("KB_ROT")) : 1);
     g_pitch = (uint32_t)pitch;
+    g_plan = &plan;
+    g_S = S;
     CK(hipMalloc(&g_scr, (size_t)512 * R * pitch));  // two-phase scratch ring (<= 512 objects)
     // KB_ALLOC=1: physically contiguous allocation (hipDeviceMallocContiguous),
     // which lets the driver map the batch with the largest page fragments
@@ -908,9 +920,75 @@ int rot_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const 
     return 0;
 }
 
+// lib:OPk_p (OP = enc | dec | ver): times the library's own launch_plan for
+// any shape, including K > 16 (the generic kernel), cold (4 rotating copies),
+// 1 MiB objects, ~1.3 GB per launch.  dec = fused decode, data {0, 1} lost.
+int lib_time(const std::string &spec, int rounds) {
+    const std::string op = spec.substr(0, 3);
+    const size_t us = spec.find('_');
+    const int k = std::atoi(spec.substr(3, us - 3).c_str()), p = std::atoi(spec.substr(us + 1).c_str());
+    const int n = k + p;
+    rsgpu_ctx *ctx;
+    if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
+    if (ctx->use_device()) { std::printf("no device\n"); return 1; }
+    std::shared_ptr<Plan> plan;
+    std::vector<uint8_t> present(n, 1);
+    if (op == "enc") plan = ctx->plan_encode();
+    else if (op == "ver") plan = ctx->plan_verify();
+    else {
+        present[0] = present[1] = 0;
+        ctx->plan_reconstruct(present.data(), false, true, plan);
+    }
+    const size_t S = ((size_t)1 << 20) / k, pitch = (S + 255) / 256 * 256, stride = (size_t)n * pitch;
+    const int nobj = (int)(((size_t)1300 << 20) / stride), NB = 4;
+    uint8_t *d;
+    uint32_t *bad;
+    CK(hipMalloc(&d, stride * nobj * NB));
+    CK(hipMalloc(&bad, nobj * 4));
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, d, stride * nobj * NB, 4242ull);
+    CK(hipDeviceSynchronize());
+    if (rsgpu_encode_dev(ctx, d, S, pitch, stride, nobj * NB, nullptr)) return 1;
+    CK(hipDeviceSynchronize());
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> ms;
+    // ~0.3 s of back-to-back launches first: the shader clock ramps up under
+    // sustained load, and VALU-heavy passes read up to 40 % slow without it
+    for (int it = 0; it < 1000; ++it)
+        CK(launch_plan(*plan, Layout{d + (size_t)(it % NB) * stride * nobj, stride, pitch, S, nobj}, bad, st));
+    CK(hipStreamSynchronize(st));
+    for (int it = 0; it < rounds + 2; ++it)
+        for (int j = 0; j < NB; ++j) {
+            CK(hipEventRecord(e0, st));
+            CK(launch_plan(*plan, Layout{d + (size_t)j * stride * nobj, stride, pitch, S, nobj}, bad, st));
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            if (it >= 2) ms.push_back(t);
+        }
+    std::vector<uint32_t> hb(nobj);
+    CK(hipMemcpy(hb.data(), bad, nobj * 4, hipMemcpyDeviceToHost));
+    for (int o = 0; o < nobj; ++o)
+        if (hb[o]) { std::printf("flagged object %d\n", o); return 1; }
+    std::sort(ms.begin(), ms.end());
+    const double med = ms[ms.size() / 2];
+    const double alg = (double)nobj * (plan->K + plan->nw) * S;
+    std::printf("lib %s: K=%d R=%d nw=%d S=%zu nobj=%d (%s kernel), med %.1f us, %.1f GB/s, %.1f%% of 8 TB/s\n",
+                spec.c_str(), plan->K, plan->R, plan->nw, S, nobj, plan->K > 16 ? "generic" : "specialised",
+                med * 1e3, alg / (med * 1e-3) / 1e9, 100.0 * alg / (med * 1e-3) / 8e12);
+    CK(hipFree(d));
+    CK(hipFree(bad));
+    return 0;
+}
+
 int main(int argc, char **argv) {
     std::string shape = argc > 1 ? argv[1] : "enc10_2";
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 20;
+    if (shape.rfind("lib:", 0) == 0) return lib_time(shape.substr(4), rounds);
     const bool sweep = shape.rfind("pitch:", 0) == 0;  // pitch:SHAPE
     if (sweep) shape = shape.substr(6);
     const bool rot = shape.rfind("rot:", 0) == 0;  // rot:SHAPE
@@ -923,7 +1001,15 @@ int main(int argc, char **argv) {
         shape = shape.substr(0, shape.find('@'));
     }
     const bool p4 = shape.find("10_4") != std::string::npos;
-    const int k = 10, p = p4 ? 4 : 2, n = k + p;
+    int k = 10, p = p4 ? 4 : 2;
+    {   // encK_P / verK_P for other code widths (K <= 16 specialised shapes)
+        const size_t us = shape.find('_');
+        if (us != std::string::npos && us > 3 && (shape.rfind("enc", 0) == 0 || shape.rfind("ver", 0) == 0)) {
+            k = std::atoi(shape.substr(3, us - 3).c_str());
+            p = std::atoi(shape.substr(us + 1).c_str());
+        }
+    }
+    const int n = k + p;
     if (obj_mib <= 0) obj_mib = p4 ? 4 : 1;
     const size_t nbytes = (size_t)(obj_mib * (1 << 20));
     int nobj = std::max(1, (int)((p4 ? 2048 : 1024) / obj_mib));
@@ -960,7 +1046,7 @@ int main(int argc, char **argv) {
         return sweep ? pitch_sweep<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str())      \
              : rot   ? rot_sweep<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str())        \
                      : run<k_, r_>(ctx, *plan, S, nobj, rounds, shape.c_str());
-    SHAPE(10, 2) SHAPE(10, 4) SHAPE(12, 2) SHAPE(12, 4) SHAPE(14, 4)
+    SHAPE(10, 2) SHAPE(10, 4) SHAPE(12, 2) SHAPE(12, 4) SHAPE(14, 4) SHAPE(16, 4) SHAPE(16, 2) SHAPE(8, 4)
 #undef SHAPE
     std::printf("no instantiation for K=%d R=%d\n", K, R);
     return 1;
