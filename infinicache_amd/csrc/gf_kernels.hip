@@ -4,9 +4,10 @@
 // reedsolomon.Encoder.Encode/Verify/Reconstruct (called from
 // /root/reference/client/ecRedis.go:390,395,406,415,420).
 //
-// Design (DESIGN.md §Kernels):
+// Design (DESIGN.md §5):
 //   * one workgroup = 256 lanes x 16 B of one object, 1D grid over
-//     (object, chunk) in linear or XCD-contiguous order (Order, gf_device.h);
+//     (object, chunk) in XCD-contiguous order (Order, gf_device.h): each XCD
+//     sweeps its own contiguous eighth of the launch;
 //   * every input row is read once with buffer_load_dwordx4 (1 KiB per wave
 //     instruction, the object base in a uniform SRD, the row offset in
 //     soffset => no per-row VALU address math);
@@ -14,8 +15,10 @@
 //     v_perm_b32 byte lookups on the 3/3/2-bit groups of the input (tables in
 //     SGPRs, from the kernarg segment) merged with v_bitop3 (3-input XOR);
 //   * rows [0, nw) are stored with buffer_store_dwordx4; rows [nw, R) are
-//     compare-to-zero rows that raise a per-object flag (fused Verify).
-// No MFMA and no LDS: the op is HBM-bound byte arithmetic.
+//     compare-to-zero rows that raise a per-object flag (fused Verify);
+//   * non-temporal loads and stores, and on passes that store rows an
+//     occupancy cap through an LDS reservation (store_lds below).
+// No MFMA and no LDS data: the op is HBM-bound byte arithmetic.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
