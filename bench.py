@@ -585,6 +585,9 @@ def main():
         "kernel": f"{kernel_key} ({dom} launches), {dom_bytes} algorithmic B/launch, "
                   f"{dom_ms * 1e3:.1f} us avg (HIP events on {len(evs)} of {args.steps} timed steps)",
         "per_kernel_GBps": {op: round(b / (ms * 1e-3) / 1e9, 1) for op, (_, b, ms) in per_op.items()},
+        # the read side alone (k*S input bytes per object and launch), SURVEY §8d
+        "read_only": {"achieved": round(nobj * k * S / (dom_ms * 1e-3) / 1e9, 1),
+                      "frac": round(nobj * k * S / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
     }
 
     warm = None
