@@ -142,21 +142,19 @@ def _as_u8(buf, writable: bool) -> Optional[np.ndarray]:
 
 
 class _ShardTable:
-    """Pointer + length arrays for a list of shards (None/empty => len 0)."""
+    """Pointer + length arrays for a list of shards (None/empty => len 0).
+    Built from raw addresses in one ctypes call each (the per-object host
+    path is latency-bound: this table is on it twice per Client.encode)."""
+
+    __slots__ = ("arrs", "ptrs", "lens")
 
     def __init__(self, shards, writable_idx=()):
-        self.arrs: List[Optional[np.ndarray]] = []
         n = len(shards)
-        self.ptrs = (_lib.u8p * n)()
-        self.lens = (ctypes.c_size_t * n)()
-        for i, s in enumerate(shards):
-            a = _as_u8(s, i in writable_idx)
-            self.arrs.append(a)
-            if a is not None and len(a):
-                self.ptrs[i] = a.ctypes.data_as(_lib.u8p)
-                self.lens[i] = len(a)
-            else:
-                self.lens[i] = 0
+        arrs = [_as_u8(s, i in writable_idx) for i, s in enumerate(shards)]
+        addrs = [a.__array_interface__["data"][0] if a is not None and len(a) else None for a in arrs]
+        self.arrs = arrs  # keeps the buffers alive for the call
+        self.ptrs = ctypes.cast((ctypes.c_void_p * n)(*addrs), _lib.u8pp)
+        self.lens = (ctypes.c_size_t * n)(*[len(a) if a is not None else 0 for a in arrs])
 
 
 def _dptr(x) -> int:
