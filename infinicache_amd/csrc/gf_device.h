@@ -52,9 +52,13 @@ template <int SAUX>
 __device__ __forceinline__ void store_row(const u32x4 &o, __amdgpu_buffer_rsrc_t rs, uint32_t voff,
                                           uint32_t soff, bool last_packed, uint32_t tail) {
     if (last_packed && tail < 16u) {
-        for (uint32_t b = 0; b < tail; ++b)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(o[b >> 2] >> (8 * (b & 3))), rs, voff + b, soff,
-                                                 SAUX);
+        for (uint32_t b = 0; b < tail; ++b) {
+            // select the dword without indexing the vector by a runtime value
+            // (that would put `o` in private memory: a scratch frame per lane)
+            const uint32_t q = b >> 2;
+            const uint32_t w = q == 0 ? o[0] : q == 1 ? o[1] : q == 2 ? o[2] : o[3];
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8 * (b & 3))), rs, voff + b, soff, SAUX);
+        }
     } else {
         __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, soff, SAUX);
     }
