@@ -436,6 +436,30 @@ std::vector<Variant> order_variants() {
     };
 }
 
+// the shipped launch (XCD order, occupancy cap) with other cache-policy bits
+template <int K, int R, int LA, int SA>
+void launch_capp(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    const int w = K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K);
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, LA, SA>), dim3(nb), dim3(256),
+                       a.p.nw ? 160u * 1024u / (unsigned)w - 256u : 0u, st, a);
+}
+template <int K, int R>
+std::vector<Variant> capp_variants() {
+    return {
+        {"shipped (nt / nt)", launch_ship<K, R>, 1, 256, false},
+        {"cap, nt / sc1 nt", launch_capp<K, R, 2, 18>, 1, 256, false},
+        {"cap, nt / sc0 sc1 nt", launch_capp<K, R, 2, 19>, 1, 256, false},
+        {"cap, nt / sc0 nt", launch_capp<K, R, 2, 3>, 1, 256, false},
+        {"cap, nt / sc1", launch_capp<K, R, 2, 16>, 1, 256, false},
+        {"cap, sc1 nt / nt", launch_capp<K, R, 18, 2>, 1, 256, false},
+        {"cap, sc0 sc1 nt / nt", launch_capp<K, R, 19, 2>, 1, 256, false},
+        {"cap, default / nt", launch_capp<K, R, 0, 2>, 1, 256, false},
+    };
+}
+
 // KB_SET=policy: cache-policy bits of loads (LA) and stores (SA); gfx950
 // buffer-op aux: 1 = sc0, 2 = nt, 16 = sc1
 template <int K, int R>
@@ -575,6 +599,7 @@ std::vector<Variant> variants() {
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "stream") return stream_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "rows") return rows_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "occ") return occ_variants<K, R>();
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "capp") return capp_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "twophase") return twophase_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "policy") return policy_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "order") return order_variants<K, R>();
