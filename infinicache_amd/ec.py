@@ -243,7 +243,7 @@ class RSEncoder:
                 if s is None or len(s) == 0:
                     if data_only and i >= self.DataShards:
                         continue
-                    bufs[i] = np.zeros(size, dtype=np.uint8)
+                    bufs[i] = np.empty(size, dtype=np.uint8)  # every byte is written
                     missing.append(i)
         return bufs, missing
 
@@ -251,21 +251,15 @@ class RSEncoder:
         if not isinstance(shards, list):
             raise InvalidArgument("shards must be a list (filled in place)")
         bufs, missing = self._prepare_missing(shards, data_only)
+        t = _ShardTable(bufs, writable_idx=missing)
+        for i in missing:
+            t.lens[i] = 0  # "missing": the buffer is the output
         n = len(shards)
-        ptrs = (_lib.u8p * n)()
-        lens = (ctypes.c_size_t * n)()
-        arrs = []
-        for i in range(n):
-            a = _as_u8(bufs[i], i in missing)
-            arrs.append(a)
-            if a is not None and len(a):
-                ptrs[i] = a.ctypes.data_as(_lib.u8p)
-                lens[i] = 0 if i in missing else len(a)
         ok = ctypes.c_int(1)
         if fused_verify:
-            _check(self._L.rsgpu_decode(self._ctx, ptrs, lens, n, ctypes.byref(ok)))
+            _check(self._L.rsgpu_decode(self._ctx, t.ptrs, t.lens, n, ctypes.byref(ok)))
         else:
-            _check(self._L.rsgpu_reconstruct(self._ctx, ptrs, lens, n, int(data_only)))
+            _check(self._L.rsgpu_reconstruct(self._ctx, t.ptrs, t.lens, n, int(data_only)))
         for i in missing:
             shards[i] = bufs[i]
         return bool(ok.value)
