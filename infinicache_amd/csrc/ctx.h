@@ -27,6 +27,7 @@ struct Slot {
     size_t cap = 0;
     hipStream_t stream = nullptr;
     uint32_t *d_bad = nullptr, *h_bad = nullptr;
+    uint32_t *m_bad = nullptr;  // device address of h_bad (mapped pinned memory)
     ~Slot() {
         if (stream) (void)hipStreamDestroy(stream);
         if (h) (void)hipHostFree(h);
@@ -269,7 +270,8 @@ struct rsgpu_ctx {
             s.reset(new Slot());
             HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
             HIP_TRY(hipMalloc(&s->d_bad, 4));
-            HIP_TRY(hipHostMalloc(&s->h_bad, 4, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc(&s->h_bad, 4, hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostGetDevicePointer((void **)&s->m_bad, s->h_bad, 0));
         }
         if (s->cap < bytes) {
             if (s->h) (void)hipHostFree(s->h);
@@ -295,4 +297,7 @@ int check_shards(const size_t *lens, int n, bool nilok, size_t *size);
 // rsgpu_host_alloc (pipeline.cpp): the per-object host API then DMAs
 // straight from / to it instead of staging through its own pinned buffer
 bool host_pinned(const void *p, size_t len);
+// the device address of such a range (kernels read/write it over PCIe), or
+// nullptr when [p, p+len) is not inside one pinned range
+void *host_device_ptr(const void *p, size_t len);
 }  // namespace rsgpu

@@ -56,7 +56,15 @@ struct Layout {
     size_t pitch;         // bytes between rows of an object
     size_t shard_len;     // bytes per shard (S)
     int nobj;
+    // one object only (nobj == 1), passes with K <= kRedirectMaxK: rows read
+    // from in_base / written to out_base (same offsets), e.g. pinned host memory
+    uint8_t *out_base = nullptr;
+    bool out_dual = false;        // written rows to base as well
+    const uint8_t *in_base = nullptr;
+    size_t in_span = 0;           // bytes readable from in_base
+    bool copy_in = false;         // input rows copied into base as well
 };
+constexpr int kRedirectMaxK = 16;  // passes that can redirect their written rows
 
 // Device workspace for mixed-pattern launches (pass images + object lists),
 // reused across calls once the previous call's kernels finished with it.

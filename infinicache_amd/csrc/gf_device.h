@@ -108,6 +108,13 @@ __device__ __forceinline__ bool wg_item(const Order &o, uint32_t &item, uint32_t
 template <int K, int R>
 struct ApplyArgs {  // one pass for every object of the launch (kernarg)
     const uint8_t *base;
+    // per-object host API (one object, rsgpu.cpp run_host): the rows may be
+    // read from / written to a caller's pinned host buffer over PCIe
+    const uint8_t *in_base;   // input rows read here (same offsets); nullptr: base
+    const uint8_t *out_base;  // written rows go here (same offsets); nullptr: base
+    uint32_t in_span;         // bytes readable from in_base (clips the tail vector)
+    uint32_t copy_in;         // with in_base: copy the input rows into base too
+    uint32_t out_dual;        // with out_base: store the written rows to base too
     uint64_t obj_stride;
     uint32_t *bad;
     uint32_t nvec;   // 16-B vectors per row
@@ -139,13 +146,28 @@ struct MultiArgs {  // per-object passes (a Get batch with mixed erasure pattern
 // (Plan::ki).  Those inputs cost one XOR instead of four v_perm + two XOR per
 // row, and one uniform branch per input (no per-coefficient branches).
 // P: Pass<K, R> (kernarg) or its constant-address-space alias (device image)
+// Zero-copy redirection of one object's rows (the per-object host API,
+// rsgpu.cpp run_host): inputs read from / outputs written to a caller's
+// pinned host buffer over PCIe, at the image's own row offsets.
+struct Redirect {
+    const uint8_t *in = nullptr;   // input rows read here; nullptr: the object base
+    uint32_t in_span = 0;          // bytes readable from `in` (the tail vector's over-read is clipped)
+    bool copy_in = false;          // also copy the input rows into the object base (image)
+    const uint8_t *out = nullptr;  // written rows go here; nullptr: the object base
+    bool dual = false;             // also store the written rows to the object base
+};
+
 template <int K, int R, int U, int BS, int LAUX, int SAUX, typename P>
 __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P &a,
                                               uint32_t nvec, uint32_t tail, uint32_t *bad,
-                                              uint32_t v0) {
+                                              uint32_t v0, const Redirect &rd = Redirect()) {
     if (v0 >= nvec) return;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsi =
+        rd.in ? __builtin_amdgcn_make_buffer_rsrc((void *)rd.in, (short)0, (int)rd.in_span, 0x00020000) : rs;
+    const __amdgpu_buffer_rsrc_t rso =
+        rd.out ? __builtin_amdgcn_make_buffer_rsrc((void *)rd.out, (short)0, (int)a.span, 0x00020000) : rs;
 
     u32x4 x[U][K];
 #pragma unroll
@@ -154,7 +176,12 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         if (U == 1 || v < nvec) {
 #pragma unroll
             for (int c = 0; c < K; ++c)
-                x[u][c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.in_off[c], LAUX);
+                x[u][c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, v * 16u, a.in_off[c], LAUX);
+            if (rd.copy_in) {
+#pragma unroll
+                for (int c = 0; c < K; ++c)
+                    store_row<SAUX>(x[u][c], rs, v * 16u, a.in_off[c], a.packed && v == nvec - 1, tail);
+            }
         }
     }
 
@@ -196,7 +223,8 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         for (int r = 0; r < R; ++r) {
             if ((uint32_t)r < a.nw) {
                 u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                store_row<SAUX>(o, rs, v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
+                store_row<SAUX>(o, rso, v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
+                if (rd.dual) store_row<SAUX>(o, rs, v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
             } else {
                 const uint32_t valid = (v == nvec - 1) ? tail : 16u;
 #pragma unroll
@@ -204,7 +232,9 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
             }
         }
     }
-    if (mismatch) atomicOr(bad + obj, 1u);
+    // every writer stores the same 1 (no atomic needed, and the flag may
+    // live in mapped host memory); zeroing happens before the launch
+    if (mismatch) bad[obj] = 1u;
     // the plan has no check rows: the pass itself clears the object's flag
     // (saves the caller's memset launch on the decode hot path)
     if (a.clear && v0 == 0) bad[obj] = 0u;
@@ -214,8 +244,14 @@ template <int K, int R, int U, int BS, int LAUX, int SAUX>
 __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
+    Redirect rd;
+    rd.in = a.in_base;
+    rd.in_span = a.in_span;
+    rd.copy_in = a.copy_in != 0;
+    rd.out = a.out_base;
+    rd.dual = a.out_dual != 0;
     gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec,
-                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x);
+                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd);
 }
 
 // Mixed erasure patterns in one launch: each workgroup reads its object's

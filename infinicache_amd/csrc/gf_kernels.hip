@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
             for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
         }
     }
-    if (mismatch) atomicOr(a.bad + obj, 1u);
+    if (mismatch) a.bad[obj] = 1u;  // same value from every writer: no atomic needed
     if (a.clear && v == 0) a.bad[obj] = 0u;
 }
 
@@ -251,6 +251,11 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
     for (int o0 = 0; o0 < L.nobj; o0 += step) {
         const int no = std::min(step, L.nobj - o0);
         a.base = L.base + (size_t)o0 * L.obj_stride;
+        a.out_base = L.out_base;  // redirection is single-object (nobj == 1, checked)
+        a.out_dual = L.out_dual ? 1u : 0u;
+        a.in_base = L.in_base;
+        a.in_span = (uint32_t)std::min<size_t>(L.in_span, 0xffffffffu);
+        a.copy_in = L.copy_in ? 1u : 0u;
         a.bad = d_bad ? d_bad + o0 : nullptr;
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
@@ -450,6 +455,9 @@ fixed_fn pick_fixed(int K, int R) {
 
 hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
     if (L.nobj <= 0 || p.R <= 0) return hipSuccess;
+    static_assert(kRedirectMaxK == kMaxK, "redirect limit");
+    if ((L.out_base || L.in_base) && (p.K > kMaxK || L.nobj != 1))
+        return hipErrorInvalidValue;  // only the specialised single-object passes redirect
     if (p.K <= kMaxK) {
         // split R into passes of <= 4 rows; written rows first, then checks
         for (int r0 = 0; r0 < p.R; r0 += kMaxR) {

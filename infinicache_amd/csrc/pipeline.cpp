@@ -71,13 +71,22 @@ int drain(rsgpu_ctx *ctx) {
     return first == hipSuccess ? RSGPU_OK : hip_fail(first, "pipeline drain");
 }
 
-// ranges pinned through this API: start -> length
+// ranges pinned through this API: start -> (length, readable length, device
+// address of start).  readable >= length: rsgpu_host_alloc's slack that
+// kernels reading the range directly may over-read into (a row's last 16-B
+// vector).
+struct PinnedRange {
+    size_t len, readable;
+    uintptr_t dev;
+};
 std::mutex g_pin_mu;
-std::map<uintptr_t, size_t> g_pinned;
+std::map<uintptr_t, PinnedRange> g_pinned;
 
-void pin_add(const void *p, size_t len) {
+void pin_add(void *p, size_t len, size_t readable) {
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) d = nullptr;
     std::lock_guard<std::mutex> g(g_pin_mu);
-    g_pinned[(uintptr_t)p] = len;
+    g_pinned[(uintptr_t)p] = {len, readable, (uintptr_t)d};
 }
 void pin_del(const void *p) {
     std::lock_guard<std::mutex> g(g_pin_mu);
@@ -93,7 +102,17 @@ bool host_pinned(const void *p, size_t len) {
     auto it = g_pinned.upper_bound(a);
     if (it == g_pinned.begin()) return false;
     --it;
-    return a >= it->first && a + len <= it->first + it->second;
+    return a >= it->first && a + len <= it->first + it->second.len;
+}
+
+void *host_device_ptr(const void *p, size_t len) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return nullptr;
+    --it;
+    if (a < it->first || a + len > it->first + it->second.readable || !it->second.dev) return nullptr;
+    return (void *)(it->second.dev + (a - it->first));
 }
 }  // namespace rsgpu
 
@@ -102,8 +121,8 @@ extern "C" {
 int rsgpu_host_register(void *p, size_t len) {
     if (!p || !len) return RSGPU_ERR_INVALID_ARG;
     if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
-    HIP_TRY(hipHostRegister(p, len, hipHostRegisterDefault));
-    pin_add(p, len);
+    HIP_TRY(hipHostRegister(p, len, hipHostRegisterMapped));
+    pin_add(p, len, len);
     return RSGPU_OK;
 }
 
@@ -118,8 +137,10 @@ int rsgpu_host_alloc(size_t len, void **out) {
     if (!out || !len) return RSGPU_ERR_INVALID_ARG;
     *out = nullptr;
     if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
-    HIP_TRY(hipHostMalloc(out, len, hipHostMallocDefault));
-    pin_add(*out, len);
+    // 64 B of slack past the caller's length: kernels may read a Split buffer
+    // in place, and a row's last 16-B vector can run past the buffer's end
+    HIP_TRY(hipHostMalloc(out, len + 64, hipHostMallocDefault));
+    pin_add(*out, len, len + 64);
     return RSGPU_OK;
 }
 

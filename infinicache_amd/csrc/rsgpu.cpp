@@ -169,7 +169,24 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     for (int c = 0; c < plan.K && split; ++c)
         split = in_src[c] == span0 + (size_t)(plan.in_rows[c] - rlo) * size;
     split = split && host_pinned(span0, span);
-    if (split) {
+    // Zero-copy inputs: a pinned Split-layout input span is read by the pass
+    // itself over PCIe (no H2D command).  The last 16-B vector of a row may
+    // run up to 15 bytes past it, so the pinned range must be readable up to
+    // rhi*size + roundup16(size) (rsgpu_host_alloc leaves that slack).  A
+    // following plan (`then`) reads the image, so the pass copies the input
+    // rows into it as well.
+    Layout L{s->d, 0, size, size, 1};
+    if (split && plan.K <= kRedirectMaxK) {
+        const size_t first = (size_t)rlo * size, need = (size_t)rhi * size + round_up(size, 16);
+        if (const uint8_t *d = (const uint8_t *)host_device_ptr(span0, need - first)) {
+            L.in_base = d - first;
+            L.in_span = need;
+            L.copy_in = then != nullptr;
+        }
+    }
+    if (L.in_base) {
+        // nothing to copy
+    } else if (split) {
         he = hipMemcpyAsync(s->d + (size_t)rlo * size, span0, span, hipMemcpyHostToDevice, s->stream);
     } else if (pin_in) {
         auto src = [&](size_t c) { return in_src[c]; };
@@ -184,28 +201,48 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         he = hipMemcpyAsync(s->d + (size_t)rlo * size, s->h + (size_t)rlo * size, span, hipMemcpyHostToDevice,
                             s->stream);
     }
-    if (he == hipSuccess && plan.nw < plan.R) he = hipMemsetAsync(s->d_bad, 0, 4, s->stream);
-    if (he == hipSuccess) he = launch_plan(plan, Layout{s->d, 0, size, size, 1}, s->d_bad, s->stream);
+    // The check flag is a mapped pinned word: zeroed here, written by the
+    // kernels over PCIe, read after the sync (no memset, no D2H command).
+    *s->h_bad = 0;
+    // Zero-copy outputs: when every written row lies in one pinned range at
+    // its Split position (row r at obase + r*size, the image's own layout),
+    // the pass stores straight into it over PCIe and the D2H commands go
+    // away.  A following plan (`then`) reads the image, so the rows are then
+    // stored to the image as well.
     std::vector<int> orows(plan.out_rows.begin(), plan.out_rows.begin() + plan.nw);
+    if (pin_out && plan.nw > 0 && plan.K <= kRedirectMaxK) {
+        const uint8_t *ob = out_dst[0] - (size_t)orows[0] * size;
+        int lo = orows[0], hi = orows[0];
+        bool split_out = true;
+        for (size_t r = 0; r < orows.size() && split_out; ++r) {
+            split_out = out_dst[r] == ob + (size_t)orows[r] * size;
+            lo = std::min(lo, orows[r]);
+            hi = std::max(hi, orows[r]);
+        }
+        if (split_out) {
+            if (uint8_t *d = (uint8_t *)host_device_ptr(ob + (size_t)lo * size, (size_t)(hi - lo + 1) * size)) {
+                L.out_base = d - (size_t)lo * size;
+                L.out_dual = then != nullptr;
+            }
+        }
+    }
+    if (he == hipSuccess) he = launch_plan(plan, L, s->m_bad, s->stream);
     auto dst = [&](size_t r) {
         return pin_out ? (const uint8_t *)out_dst[r] : (const uint8_t *)s->h + (size_t)orows[r] * size;
     };
-    for (size_t i = 0; i < orows.size() && he == hipSuccess;) {
+    for (size_t i = 0; i < orows.size() && he == hipSuccess && !L.out_base;) {
         const size_t j = run_end(orows, i, dst);
         he = hipMemcpyAsync((void *)dst(i), s->d + (size_t)orows[i] * size, (j - i) * size,
                             hipMemcpyDeviceToHost, s->stream);
         i = j;
     }
-    if (he == hipSuccess && plan.nw < plan.R)
-        he = hipMemcpyAsync(s->h_bad, s->d_bad, 4, hipMemcpyDeviceToHost, s->stream);
     if (then && he == hipSuccess) {  // check-only plan (nw == 0) on the image as it stands
         // the first plan has no check rows (run_host's contract with `then`):
         // its pass already cleared the flag.  (Running the written rows' D2H
         // on a side stream to overlap this kernel was measured slower: 67.5 ->
         // 85.7 us per fused encode+verify; the cross-stream event and second
         // sync cost more than the overlap.)
-        he = launch_plan(*then, Layout{s->d, 0, size, size, 1}, s->d_bad, s->stream);
-        if (he == hipSuccess) he = hipMemcpyAsync(s->h_bad, s->d_bad, 4, hipMemcpyDeviceToHost, s->stream);
+        he = launch_plan(*then, Layout{s->d, 0, size, size, 1}, s->m_bad, s->stream);
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
     if (he != hipSuccess) {
