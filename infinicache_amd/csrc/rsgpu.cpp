@@ -127,8 +127,12 @@ namespace {
 // D2H, the check flag.  The device image is byte-packed (row i at i*size, the
 // pass's packed mode, gf_device.h store_row), so host rows move as plain 1D
 // copies with no device-side repack:
-//   * inputs inside one range pinned with rsgpu_host_register / _alloc at
-//     base + row*size (Split's layout) go as ONE DMA of the row span;
+//   * inputs inside one pinned range at base + row*size (Split's layout) are
+//     read by the pass itself over PCIe (zero-copy, no H2D command) when the
+//     range is readable up to the last row's final 16-B vector, else go as
+//     ONE DMA of the row span;
+//   * written rows at their Split positions in one pinned range are stored
+//     by the pass straight into it (zero-copy, no D2H command);
 //   * other pinned rows go as one DMA per run of rows consecutive in both the
 //     object and host memory;
 //   * pageable rows are staged into the slot's pinned buffer (same packed
