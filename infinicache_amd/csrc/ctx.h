@@ -24,6 +24,7 @@ namespace rsgpu {
 // of an object laid out [row][pitch], a stream and a mismatch flag.
 struct Slot {
     uint8_t *h = nullptr, *d = nullptr;
+    uint8_t *hdev = nullptr;  // device address of the pinned staging image h
     size_t cap = 0;
     hipStream_t stream = nullptr;
     uint32_t *d_bad = nullptr, *h_bad = nullptr;
@@ -276,9 +277,10 @@ struct rsgpu_ctx {
         if (s->cap < bytes) {
             if (s->h) (void)hipHostFree(s->h);
             if (s->d) (void)hipFree(s->d);
-            s->h = nullptr; s->d = nullptr; s->cap = 0;
+            s->h = nullptr; s->d = nullptr; s->hdev = nullptr; s->cap = 0;
             const size_t cap = round_up(bytes, (size_t)1 << 20);
             HIP_TRY(hipHostMalloc(&s->h, cap, hipHostMallocDefault));
+            HIP_TRY(hipHostGetDevicePointer((void **)&s->hdev, s->h, 0));
             HIP_TRY(hipMalloc(&s->d, cap));
             s->cap = cap;
         }

@@ -202,8 +202,16 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         }
     } else {
         for (int c = 0; c < plan.K; ++c) std::memcpy(s->h + (size_t)plan.in_rows[c] * size, in_src[c], size);
-        he = hipMemcpyAsync(s->d + (size_t)rlo * size, s->h + (size_t)rlo * size, span, hipMemcpyHostToDevice,
-                            s->stream);
+        if (plan.K <= kRedirectMaxK && s->hdev) {
+            // the pass reads the pinned staging image in place (zero-copy);
+            // the slot holds nrows_staged*size + 16 bytes at least
+            L.in_base = s->hdev;
+            L.in_span = (size_t)rhi * size + round_up(size, 16);
+            L.copy_in = then != nullptr;
+        } else {
+            he = hipMemcpyAsync(s->d + (size_t)rlo * size, s->h + (size_t)rlo * size, span,
+                                hipMemcpyHostToDevice, s->stream);
+        }
     }
     // The check flag is a mapped pinned word: zeroed here, written by the
     // kernels over PCIe, read after the sync (no memset, no D2H command).
@@ -229,6 +237,11 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
                 L.out_dual = then != nullptr;
             }
         }
+    } else if (!pin_out && plan.nw > 0 && plan.K <= kRedirectMaxK && s->hdev) {
+        // pageable outputs: the pass stores into the pinned staging image in
+        // place (zero-copy), copied out to the caller after the sync
+        L.out_base = s->hdev;
+        L.out_dual = then != nullptr;
     }
     if (he == hipSuccess) he = launch_plan(plan, L, s->m_bad, s->stream);
     auto dst = [&](size_t r) {
