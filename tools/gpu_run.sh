@@ -34,7 +34,7 @@ for s in $STEPS; do
     kbench) for sh in ${KSHAPES:-enc10_2 dec10_2 enc10_4 rdata10_4 decx10_4 ver10_2 ver10_4}; do
               run kbench_$sh 300 ./tools/kbench $sh 15
             done ;;
-    lat)    run lat_bench 300 ./tools/lat_bench 300 ;;
+    lat)    run lat_bench 300 ./tools/lat_bench 300 2 ;;
     cpuinfo) (nproc; grep -m1 "model name" /proc/cpuinfo; grep -o -w -e avx512bw -e avx2 -e gfni /proc/cpuinfo | sort | uniq -c; cat /sys/fs/cgroup/cpu.max) > gpurun_out/cpuinfo.log 2>&1 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 ;;
     pmc_all) for wl in enc dec4; do

@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include <time.h>
 
 #include "rsgpu.h"
@@ -32,6 +33,63 @@ static double pct(double *v, int n, double p) {
     qsort(v, n, sizeof(double), cmp);
     int i = (int)(p * (n - 1) + 0.5);
     return v[i];
+}
+
+/* Concurrent callers (many EcSet/EcGet in flight, as a client serving many
+ * requests would issue): T threads, each with its own pinned Split buffer,
+ * run fused encode+verify then decode on 1 MiB objects for `secs` seconds;
+ * prints the aggregate object rate. */
+struct conc_arg {
+    rsgpu_ctx *ctx;
+    double secs;
+    long done;
+    int err;
+};
+
+static void *conc_worker(void *vp) {
+    struct conc_arg *a = (struct conc_arg *)vp;
+    const int k = 10, p = 2, n = k + p;
+    const size_t nb = 1 << 20, S = (nb + k - 1) / k;
+    uint8_t *buf = NULL;
+    if (rsgpu_host_alloc(n * S, (void **)&buf)) { a->err = 1; return NULL; }
+    for (size_t i = 0; i < k * S; ++i) buf[i] = (uint8_t)(i * 131 + 7);
+    uint8_t *sh[12];
+    size_t lens[12];
+    for (int i = 0; i < n; ++i) sh[i] = buf + i * S;
+    const double t0 = now_us();
+    while (now_us() - t0 < a->secs * 1e6) {
+        int ok = 0;
+        for (int i = 0; i < n; ++i) lens[i] = S;
+        if (rsgpu_encode_verify(a->ctx, sh, lens, n, &ok) || !ok) { a->err = 2; break; }
+        lens[0] = lens[5] = 0;
+        if (rsgpu_decode(a->ctx, sh, lens, n, &ok) || !ok) { a->err = 3; break; }
+        a->done += 1;
+    }
+    rsgpu_host_free(buf);
+    return NULL;
+}
+
+static int concurrent(rsgpu_ctx *ctx, int threads, double secs) {
+    pthread_t th[64];
+    struct conc_arg args[64];
+    if (threads > 64) threads = 64;
+    const double t0 = now_us();
+    for (int t = 0; t < threads; ++t) {
+        args[t] = (struct conc_arg){ctx, secs, 0, 0};
+        pthread_create(&th[t], NULL, conc_worker, &args[t]);
+    }
+    long done = 0;
+    int err = 0;
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL);
+        done += args[t].done;
+        err |= args[t].err;
+    }
+    const double el = (now_us() - t0) * 1e-6;
+    printf("concurrent %2d threads: %7.0f objects/s (encode+verify and decode each), %6.2f GiB/s of object "
+           "bytes per op pair%s\n", threads, done / el, 2.0 * done * (1 << 20) / el / (1 << 30),
+           err ? "  ERROR" : "");
+    return err;
 }
 
 int main(int argc, char **argv) {
@@ -84,6 +142,9 @@ int main(int argc, char **argv) {
         if (pinned) rsgpu_host_free(buf); else free(buf);
         free(keep);
     }
+    int err = 0;
+    if (argc > 2)  /* ./lat_bench ITERS CONC_SECONDS: concurrent callers too */
+        for (int t = 1; t <= 16; t *= 2) err |= concurrent(ctx, t, atof(argv[2]));
     rsgpu_destroy(ctx);
-    return 0;
+    return err ? 7 : 0;
 }
