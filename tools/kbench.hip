@@ -203,6 +203,38 @@ void launch_m(const void *, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((gf_apply_multi<K, R, 1, 256, 2, 2, CH>), dim3(nb), dim3(256), 0, st, m);
 }
 
+// the mixed-pattern kernel under an occupancy cap of W workgroups per CU
+// (W = 0: the library's store_lds(K) cap)
+template <int K, int R, int W>
+void launch_mc(const void *, dim3 grid, hipStream_t st) {
+    MultiArgs<K, R> m = *(const MultiArgs<K, R> *)g_multi_args;
+    unsigned nb;
+    m.ord = order_for<0>(grid, (size_t)grid.y * m.obj_stride, nb);
+    const int w = W ? W : (K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K));
+    hipLaunchKernelGGL((gf_apply_multi<K, R, 1, 256, 2, 2, 1>), dim3(nb), dim3(256),
+                       160u * 1024u / (unsigned)w - 256u, st, m);
+}
+// the same with the pass read through the kernarg-fetched pointer but the
+// object / pass index of the item computed, not loaded (isolates the first
+// scalar load of the chain)
+template <int K, int R, int W>
+__global__ __launch_bounds__(256) void apply_cpass_cap(const MultiArgs<K, R> m) {
+    uint32_t obj, chunk;
+    if (!wg_item(m.ord, obj, chunk)) return;
+    const __attribute__((address_space(4))) Pass<K, R> &p = *((constant_ptr<Pass<K, R>>)m.passes);
+    gf_apply_body<K, R, 1, 256, 2, 2>(m.base + (uint64_t)obj * m.obj_stride, obj, p, m.nvec, m.tail,
+                                       m.bad, chunk * 256 + threadIdx.x);
+}
+template <int K, int R, int W>
+void launch_cpc(const void *, dim3 grid, hipStream_t st) {
+    MultiArgs<K, R> m = *(const MultiArgs<K, R> *)g_multi_args;
+    unsigned nb;
+    m.ord = order_for<0>(grid, (size_t)grid.y * m.obj_stride, nb);
+    const int w = W ? W : (K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K));
+    hipLaunchKernelGGL((apply_cpass_cap<K, R, W>), dim3(nb), dim3(256), 160u * 1024u / (unsigned)w - 256u,
+                       st, m);
+}
+
 // one workgroup walks CH consecutive chunks of its object (longer
 // sequential runs per DRAM page for each of the K+R row streams)
 template <int K, int R, int CH>
@@ -385,6 +417,23 @@ std::vector<Variant> rows_variants() {
         {"shipped", launch_ship<K, R>, 1, 256, false},
         {"encode's row layout", launch_rows<K, R, 0>, 1, 256, true},
         {"decode's row layout", launch_rows<K, R, 1>, 1, 256, true},
+    };
+}
+
+// KB_SET=multi: cost of the mixed-pattern kernel's per-workgroup lookups
+// (object index, pass index, then the pass) on a uniform pattern, and its
+// occupancy cap
+template <int K, int R>
+std::vector<Variant> multi_variants() {
+    return {
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"device pass, library cap", launch_cpc<K, R, 0>, 1, 256, false},
+        {"multi, library cap", launch_mc<K, R, 0>, 1, 256, false},
+        {"multi, cap 2", launch_mc<K, R, 2>, 1, 256, false},
+        {"multi, cap 6", launch_mc<K, R, 6>, 1, 256, false},
+        {"multi, cap 8", launch_mc<K, R, 8>, 1, 256, false},
+        {"multi, cap 12", launch_mc<K, R, 12>, 1, 256, false},
+        {"multi, full occupancy", launch_m<K, R, 1>, 1, 256, false},
     };
 }
 
@@ -598,6 +647,7 @@ template <int K, int R>
 std::vector<Variant> variants() {
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "stream") return stream_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "rows") return rows_variants<K, R>();
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "multi") return multi_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "occ") return occ_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "capp") return capp_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "twophase") return twophase_variants<K, R>();
