@@ -119,7 +119,10 @@ struct ApplyArgs {  // one pass for every object of the launch (kernarg)
     uint32_t *bad;
     uint32_t nvec;   // 16-B vectors per row
     uint32_t tail;   // valid bytes in the last vector (1..16)
-    Order ord;       // item = object
+    uint32_t opw;    // objects per workgroup (> 1: small objects, item = group of opw)
+    uint32_t nobj;   // objects in the launch (bounds the last group when opw > 1)
+    uint32_t gspan;  // opw > 1: bytes a group's objects cover from the first one's base
+    Order ord;       // item = object, or group of opw objects
     Pass<K, R> p;
 };
 
@@ -157,13 +160,18 @@ struct Redirect {
     bool dual = false;             // also store the written rows to the object base
 };
 
+// Small objects (ApplyArgs::opw > 1): a workgroup codes several whole
+// objects, lane -> (object, vector); `ob` is then the first object's base
+// (uniform), `lane_off` the lane's object offset from it and `span` the bytes
+// the group's objects cover.
 template <int K, int R, int U, int BS, int LAUX, int SAUX, typename P>
 __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P &a,
                                               uint32_t nvec, uint32_t tail, uint32_t *bad,
-                                              uint32_t v0, const Redirect &rd = Redirect()) {
+                                              uint32_t v0, const Redirect &rd = Redirect(),
+                                              uint32_t lane_off = 0, uint32_t span = 0) {
     if (v0 >= nvec) return;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)(span ? span : a.span), 0x00020000);
     const __amdgpu_buffer_rsrc_t rsi =
         rd.in ? __builtin_amdgcn_make_buffer_rsrc((void *)rd.in, (short)0, (int)rd.in_span, 0x00020000) : rs;
     const __amdgpu_buffer_rsrc_t rso =
@@ -176,11 +184,11 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         if (U == 1 || v < nvec) {
 #pragma unroll
             for (int c = 0; c < K; ++c)
-                x[u][c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, v * 16u, a.in_off[c], LAUX);
+                x[u][c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, lane_off + v * 16u, a.in_off[c], LAUX);
             if (rd.copy_in) {
 #pragma unroll
                 for (int c = 0; c < K; ++c)
-                    store_row<SAUX>(x[u][c], rs, v * 16u, a.in_off[c], a.packed && v == nvec - 1, tail);
+                    store_row<SAUX>(x[u][c], rs, lane_off + v * 16u, a.in_off[c], a.packed && v == nvec - 1, tail);
             }
         }
     }
@@ -223,8 +231,8 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         for (int r = 0; r < R; ++r) {
             if ((uint32_t)r < a.nw) {
                 u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                store_row<SAUX>(o, rso, v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
-                if (rd.dual) store_row<SAUX>(o, rs, v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
+                store_row<SAUX>(o, rso, lane_off + v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
+                if (rd.dual) store_row<SAUX>(o, rs, lane_off + v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
             } else {
                 const uint32_t valid = (v == nvec - 1) ? tail : 16u;
 #pragma unroll
@@ -244,6 +252,14 @@ template <int K, int R, int U, int BS, int LAUX, int SAUX>
 __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
+    if (a.opw > 1) {  // small objects: lane -> (object j of the group, vector v)
+        const uint32_t j = threadIdx.x / a.nvec, o0 = obj * a.opw;
+        if (j >= a.opw || o0 + j >= a.nobj) return;
+        gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)o0 * a.obj_stride, o0 + j, a.p, a.nvec,
+                                               a.tail, a.bad, threadIdx.x - j * a.nvec, Redirect(),
+                                               j * (uint32_t)a.obj_stride, a.gspan);
+        return;
+    }
     Redirect rd;
     rd.in = a.in_base;
     rd.in_span = a.in_span;

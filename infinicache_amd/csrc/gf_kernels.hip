@@ -247,6 +247,36 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
     a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
     fill_pass<K, R>(p, s, L.pitch, a.nvec, d_bad != nullptr, a.p);
     const unsigned gx = (a.nvec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
+    // Small objects (a row of at most half a workgroup's vectors): one
+    // workgroup codes opw whole objects, so its lanes stay busy (1 KiB
+    // objects: 7 of 256 lanes otherwise).  The group's objects must lie in
+    // one 32-bit buffer range.
+    a.opw = 1;
+    a.nobj = 0;
+    a.gspan = 0;
+    if (L.nobj > 1 && !L.in_base && !L.out_base && kUnroll == 1 && a.nvec * 2 <= kBlock) {
+        uint32_t opw = kBlock / a.nvec;
+        while (opw > 1 && (uint64_t)(opw - 1) * L.obj_stride + a.p.span >= 0xffffffffull) opw /= 2;
+        if (opw > 1) {
+            a.opw = opw;
+            a.gspan = (uint32_t)((uint64_t)(opw - 1) * L.obj_stride + a.p.span);
+            const int groups = (L.nobj + (int)opw - 1) / (int)opw;
+            for (int g0 = 0; g0 < groups; g0 += max_items(1)) {
+                const int ng = std::min(max_items(1), groups - g0);
+                const size_t o0 = (size_t)g0 * opw;
+                a.base = L.base + o0 * L.obj_stride;
+                a.bad = d_bad ? d_bad + o0 : nullptr;
+                a.nobj = (uint32_t)std::min<size_t>((size_t)ng * opw, (size_t)L.nobj - o0);
+                unsigned grid;
+                a.ord = make_order(1, (uint32_t)ng, (size_t)a.nobj * L.obj_stride, grid);
+                hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
+                                   dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+            }
+            return hipSuccess;
+        }
+    }
     const int step = max_items(gx);
     for (int o0 = 0; o0 < L.nobj; o0 += step) {
         const int no = std::min(step, L.nobj - o0);

@@ -444,6 +444,67 @@ def test_dev_many_objects_grid_y_split(gpu):
             assert np.array_equal(h[o, k + r], want[r]), o
 
 
+@pytest.mark.parametrize("k,p,S,nobj,gap", [(10, 2, 103, 1001, 0), (10, 2, 410, 257, 48), (10, 4, 1, 700, 0),
+                                            (10, 2, 17, 513, 16), (12, 4, 2048, 33, 0), (10, 2, 2049, 9, 0),
+                                            (3, 1, 1000, 100, 4096)])
+def test_dev_small_objects_packed_workgroups(gpu, k, p, S, nobj, gap):
+    """Rows of <= 128 vectors: a workgroup codes 256 // nvec whole objects
+    (gf_kernels.hip launch_fixed, opw > 1).  Encode the whole batch against
+    the oracle, per-object Verify flags, fused decode and data-only
+    reconstruct; ragged last group, strides with gaps between objects."""
+    n = k + p
+    pitch = (S + 15) // 16 * 16
+    stride = n * pitch + gap
+    g = torch.Generator(device="cuda").manual_seed(S * 7 + nobj)
+    flat = torch.randint(0, 256, (nobj * stride,), dtype=torch.uint8, device="cuda", generator=g)
+    b = flat.view(nobj, stride)
+    for i in range(n):  # zero pads: written rows' [S, roundup16(S)) get the pads' coding (rsgpu.h)
+        b[:, i * pitch + S:(i + 1) * pitch] = 0
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    before = b.cpu().numpy().copy()
+    enc.encode_dev(flat, S, pitch, stride, nobj, s)
+    torch.cuda.synchronize()
+    h = b.cpu().numpy()
+    ref = before.copy()
+    m = enc.matrix()
+    oracle.code_batch(m[k:], list(range(k)), list(range(k, n)), ref.reshape(-1), stride, pitch, S, nobj,
+                      nthreads=8)
+    rows = h[:, :n * pitch].reshape(nobj, n, pitch)
+    assert np.array_equal(rows[:, :, :S], ref[:, :n * pitch].reshape(nobj, n, pitch)[:, :, :S])
+    # nothing outside the parity rows changed (data rows, gaps between objects)
+    mask = np.ones(stride, bool)
+    for r in range(k, n):
+        mask[r * pitch:r * pitch + S] = False
+    assert np.array_equal(h[:, mask], before[:, mask])
+    # Verify: flags land on exactly the corrupted objects
+    hit = sorted({0, nobj - 1, nobj // 2, min(nobj - 1, 255)})
+    for o in hit:
+        b[o, (o % n) * pitch + (o * 13) % S] ^= 0x5A
+    bad = torch.full((nobj,), 3, dtype=torch.int32, device="cuda")
+    enc.verify_dev(flat, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit
+    for o in hit:
+        b[o, (o % n) * pitch + (o * 13) % S] ^= 0x5A
+    golden = b.clone()
+    # fused decode with two lost data rows (or the one row of a k=3 code)
+    lost = (0, k // 2) if p >= 2 else (1,)
+    present = [i not in lost for i in range(n)]
+    for i in lost:
+        b[:, i * pitch:i * pitch + S] = 0xC3
+    bad.fill_(5)
+    enc.decode_dev(flat, present, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert int(bad.sum()) == 0
+    assert torch.equal(b, golden)
+    for i in lost:
+        b[:, i * pitch:i * pitch + S] = 0x3C
+    enc.reconstruct_dev(flat, present, S, pitch, stride, nobj, data_only=True, stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(b, golden)
+
+
 # --------------------------------------------- batched host-memory pipeline
 
 @pytest.mark.parametrize("pinned", [False, True])

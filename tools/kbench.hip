@@ -998,7 +998,12 @@ int rot_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const 
 // lib:OPk_p (OP = enc | dec | ver): times the library's own launch_plan for
 // any shape, including K > 16 (the generic kernel), cold (4 rotating copies),
 // 1 MiB objects, ~1.3 GB per launch.  dec = fused decode, data {0, 1} lost.
-int lib_time(const std::string &spec, int rounds) {
+int lib_time(std::string spec, int rounds) {
+    double obj_mib = 1;  // lib:OPk_p@M: object size M MiB (fractions allowed)
+    if (spec.find('@') != std::string::npos) {
+        obj_mib = std::atof(spec.substr(spec.find('@') + 1).c_str());
+        spec = spec.substr(0, spec.find('@'));
+    }
     const std::string op = spec.substr(0, 3);
     const size_t us = spec.find('_');
     const int k = std::atoi(spec.substr(3, us - 3).c_str()), p = std::atoi(spec.substr(us + 1).c_str());
@@ -1014,7 +1019,10 @@ int lib_time(const std::string &spec, int rounds) {
         present[0] = present[1] = 0;
         ctx->plan_reconstruct(present.data(), false, true, plan);
     }
-    const size_t S = ((size_t)1 << 20) / k, pitch = (S + 255) / 256 * 256, stride = (size_t)n * pitch;
+    const size_t nbytes = (size_t)(obj_mib * (1 << 20)), S = (nbytes + k - 1) / k;
+    // pitch: S rounded to 16 B (the smallest the layout allows) below 4 KiB
+    // shards, else to 256 B as the bench batches
+    const size_t pitch = S < 4096 ? (S + 15) / 16 * 16 : (S + 255) / 256 * 256, stride = (size_t)n * pitch;
     const int nobj = (int)(((size_t)1300 << 20) / stride), NB = 4;
     uint8_t *d;
     uint32_t *bad;
@@ -1052,9 +1060,10 @@ int lib_time(const std::string &spec, int rounds) {
     std::sort(ms.begin(), ms.end());
     const double med = ms[ms.size() / 2];
     const double alg = (double)nobj * (plan->K + plan->nw) * S;
-    std::printf("lib %s: K=%d R=%d nw=%d S=%zu nobj=%d (%s kernel), med %.1f us, %.1f GB/s, %.1f%% of 8 TB/s\n",
-                spec.c_str(), plan->K, plan->R, plan->nw, S, nobj, plan->K > 16 ? "generic" : "specialised",
+    std::printf("lib %s@%g: K=%d R=%d nw=%d S=%zu nobj=%d (%s kernel), med %.1f us, %.1f GB/s, %.1f%% of 8 TB/s\n",
+                spec.c_str(), obj_mib, plan->K, plan->R, plan->nw, S, nobj, plan->K > 16 ? "generic" : "specialised",
                 med * 1e3, alg / (med * 1e-3) / 1e9, 100.0 * alg / (med * 1e-3) / 8e12);
+    std::fflush(stdout);
     CK(hipFree(d));
     CK(hipFree(bad));
     return 0;
