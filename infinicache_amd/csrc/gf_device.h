@@ -271,9 +271,10 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
 }
 
 // Mixed erasure patterns in one launch: each workgroup reads its object's
-// pass index (uniform) and then the pass itself through scalar loads — two
-// dependent loads before its first data load, so a workgroup walks CH chunks
-// of its object with the pass kept in SGPRs to amortise them.
+// pass index (uniform) and then the pass itself through scalar loads.  CH > 1
+// walks several chunks of the object per workgroup with the pass kept in
+// SGPRs; the product uses CH = 1 (the lookups cost nothing measurable,
+// tools/kbench KB_SET=multi, and longer walks were slower).
 template <typename T>
 using constant_ptr = const __attribute__((address_space(4))) T *;
 
