@@ -900,7 +900,7 @@ template <int K, int R>
 int pitch_sweep(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *shape) {
     // every buffer is revisited only after the other pads' buffers (>= 9 GB of
     // traffic), so this sweep is cold
-    const std::vector<size_t> pads = {0, 128, 256, 512, 768, 1024, 1536, 2048, 3072, 4096, 8192};
+    const std::vector<size_t> pads = {0, 16, 64, 128, 256, 512, 1024, 2048, 3072, 4096, 4352, 8192, 65792};
     const int np = (int)pads.size();
     std::vector<uint8_t *> bufs;
     std::vector<ApplyArgs<K, R>> args;
