@@ -269,6 +269,10 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
                 a.nobj = (uint32_t)std::min<size_t>((size_t)ng * opw, (size_t)L.nobj - o0);
                 unsigned grid;
                 a.ord = make_order(1, (uint32_t)ng, (size_t)a.nobj * L.obj_stride, grid);
+                // (staging the group through LDS so that every wave load is
+                // ~1 KiB of consecutive rows measured +6 points at 1 KiB
+                // encode, 0 on decode and -7 / -4 points at 4 / 16 KiB:
+                // tools/kbench KB_SET=small, not shipped)
                 hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
                                    dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
                 hipError_t e = hipGetLastError();
