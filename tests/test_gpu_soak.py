@@ -1,0 +1,250 @@
+"""Time-bounded randomized soak of the HIP path against the CPU oracle
+(oracle/, the restatement of klauspost/reedsolomon v1.9.3).  Off by default:
+set RSGPU_SOAK_SECONDS (e.g. 240) to run it on the MI355X box; the regular
+`-m gpu` suite skips it.  Each iteration draws one case from a wider space
+than tests/test_gpu_random.py:
+  * host ops (encode, encode_verify, verify, reconstruct, rdata, decode,
+    update) with up to 40 data and 10 parity shards (the generic K > 16
+    kernel) and both matrix kinds;
+  * device batches: encode vs the oracle's batch port, per-object Verify
+    flags after random corruption, fused decode (uniform pattern), mixed
+    per-object patterns, ReconstructData; shard sizes from 1 B (packed
+    small-object workgroups) to 40 KB, gaps between objects;
+  * pinned Split buffers (zero-copy passes) for every per-object op.
+Every result is compared bit-exact (bytes) or exactly (booleans, error
+classes) with the oracle on the same input.  Prints a per-kind case count."""
+import collections
+import ctypes
+import os
+import time
+
+import numpy as np
+import pytest
+
+import infinicache_amd as ia
+import oracle
+
+SECONDS = float(os.environ.get("RSGPU_SOAK_SECONDS", "0"))
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(SECONDS <= 0, reason="set RSGPU_SOAK_SECONDS to run the soak")]
+
+
+def _size(rng, hi=40000):
+    return int(rng.choice([1, 2, 15, 16, 17, 100, 103, 255, 410, 1023, 2048, 2049, 4097,
+                           int(rng.integers(1, hi))]))
+
+
+def _host_case(rng, counts):
+    k = int(rng.integers(1, 41))
+    p = int(rng.integers(1, 11))
+    n = k + p
+    size = _size(rng, 20000)
+    kind = str(rng.choice(["vandermonde", "cauchy"]))
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    e, full = oracle.encode(k, p, data + [bytes(size)] * p, kind)
+    assert e == 0
+    enc = ia.New(k, p, matrix=kind)
+    op = str(rng.choice(["encode", "encode_verify", "verify", "reconstruct", "rdata", "decode", "update"]))
+    tag = ("host", op, k, p, size, kind)
+    counts["host_" + op] += 1
+    if op in ("encode", "encode_verify"):
+        sh = [full[i].copy() for i in range(k)] + [np.full(size, 0x6B, np.uint8) for _ in range(p)]
+        if op == "encode":
+            enc.Encode(sh)
+        else:
+            assert enc.EncodeVerify(sh), tag
+        for r in range(k, n):
+            assert np.array_equal(sh[r], full[r]), tag
+    elif op == "verify":
+        sh = [s.copy() for s in full]
+        if rng.random() < 0.5:
+            sh[int(rng.integers(0, n))][int(rng.integers(0, size))] ^= int(rng.integers(1, 256))
+        e, want = oracle.verify(k, p, sh, kind)
+        assert e == 0 and enc.Verify(sh) == want, tag
+    elif op == "update":
+        sh = [s.copy() for s in full]
+        newd = [None] * k
+        for c in rng.choice(k, int(rng.integers(1, k + 1)), replace=False).tolist():
+            newd[c] = rng.integers(0, 256, size, dtype=np.uint8)
+        e, want = oracle.update(k, p, [s.copy() for s in full], newd, kind)
+        assert e == 0
+        enc.Update(sh, newd)
+        for i in range(n):
+            assert np.array_equal(sh[i], want[i]), (tag, i)
+    else:
+        lost = sorted(rng.choice(n, int(rng.integers(1, p + 1)), replace=False).tolist())
+        src = [s.copy() for s in full]
+        if rng.random() < 0.3:
+            src[int(rng.integers(0, n))][int(rng.integers(0, size))] ^= 0x81
+        sh = [None if i in lost else src[i].copy() for i in range(n)]
+        ref = [None if i in lost else src[i].copy() for i in range(n)]
+        e, want = oracle.reconstruct(k, p, ref, kind, data_only=(op == "rdata"))
+        assert e == 0
+        if op == "decode":
+            ok = enc.DecodeVerify(sh)
+            e2, want_ok = oracle.verify(k, p, want, kind)
+            assert e2 == 0 and ok == want_ok, tag
+        else:
+            (enc.ReconstructData if op == "rdata" else enc.Reconstruct)(sh)
+        for i in range(n):
+            if op == "rdata" and i >= k and i in lost:
+                assert sh[i] is None, tag
+                continue
+            assert np.array_equal(sh[i], want[i]), (tag, lost, i)
+
+
+def _device_case(rng, counts):
+    import torch
+    k = int(rng.integers(1, 31))
+    p = int(rng.integers(1, 9))
+    n = k + p
+    S = _size(rng, 40000)
+    pitch = (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+    gap = 16 * int(rng.integers(0, 8))
+    stride = n * pitch + gap
+    nobj = int(rng.integers(1, max(2, min(400, (24 << 20) // stride))))
+    kind = str(rng.choice(["vandermonde", "cauchy"]))
+    enc = ia.New(k, p, matrix=kind)
+    m = enc.matrix()
+    host = rng.integers(0, 256, (nobj, stride), dtype=np.uint8)
+    for i in range(n):  # zero pads (written rows' pads get the pads' coding)
+        host[:, i * pitch + S:(i + 1) * pitch] = 0
+    buf = torch.from_numpy(host.copy()).cuda()
+    st = torch.cuda.current_stream()
+    tag = ("dev", k, p, S, pitch, gap, nobj, kind)
+    enc.encode_dev(buf, S, pitch, stride, nobj, st)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    ref = host.copy()
+    oracle.code_batch(m[k:], list(range(k)), list(range(k, n)), ref.reshape(-1), stride, pitch, S, nobj,
+                      nthreads=8)
+    assert np.array_equal(got, ref), tag
+    counts["dev_encode"] += 1
+    coded = got.copy()
+    op = str(rng.choice(["verify", "decode", "multi", "rdata"]))
+    counts["dev_" + op] += 1
+    if op == "verify":
+        hit = sorted(set(rng.integers(0, nobj, int(rng.integers(0, min(nobj, 6) + 1))).tolist()))
+        for o in hit:
+            r = int(rng.integers(0, n))
+            got[o, r * pitch + int(rng.integers(0, S))] ^= int(rng.integers(1, 256))
+        buf = torch.from_numpy(got).cuda()
+        bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+        enc.verify_dev(buf, S, pitch, stride, nobj, bad, st)
+        torch.cuda.synchronize()
+        assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit, tag
+        return
+    if op == "multi":
+        pres = np.ones((nobj, n), dtype=np.uint8)
+        for o in range(nobj):
+            pres[o, rng.choice(n, int(rng.integers(1, p + 1)), replace=False)] = 0
+    else:
+        row = np.ones(n, dtype=np.uint8)
+        row[rng.choice(n, int(rng.integers(1, p + 1)), replace=False)] = 0
+        pres = np.tile(row, (nobj, 1))
+    for o in range(nobj):
+        for i in range(n):
+            if not pres[o, i]:
+                got[o, i * pitch:i * pitch + S] = rng.integers(0, 256, S, dtype=np.uint8)
+    buf = torch.from_numpy(got.copy()).cuda()
+    bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    if op == "multi":
+        enc.decode_dev_multi(buf, pres, S, pitch, stride, nobj, bad, st)
+    elif op == "decode":
+        enc.decode_dev(buf, [bool(x) for x in pres[0]], S, pitch, stride, nobj, bad, st)
+    else:
+        enc.reconstruct_dev(buf, [bool(x) for x in pres[0]], S, pitch, stride, nobj, data_only=True,
+                            stream=st)
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    if op != "rdata":
+        assert int(bad.sum()) == 0, tag
+    for o in range(nobj):
+        for i in range(n):
+            if op == "rdata" and i >= k and not pres[o, i]:
+                continue  # parity left as it was
+            a = out[o, i * pitch:i * pitch + S]
+            assert np.array_equal(a, coded[o, i * pitch:i * pitch + S]), (tag, op, o, i)
+    # bytes outside the rebuilt rows' valid ranges are untouched (gaps, pads of other rows)
+    assert np.array_equal(out[:, n * pitch:], got[:, n * pitch:]), tag
+
+
+def _call(enc, fn, bufs, lens, *extra):
+    n = len(bufs)
+    from infinicache_amd import _lib
+    ptrs = ctypes.cast((ctypes.c_void_p * n)(*[b.__array_interface__["data"][0] for b in bufs]), _lib.u8pp)
+    return getattr(enc._L, fn)(enc._ctx, ptrs, (ctypes.c_size_t * n)(*lens), n, *extra)
+
+
+def _pinned_case(rng, counts):
+    k = int(rng.integers(1, 17))
+    p = int(rng.integers(1, 5))
+    n = k + p
+    size = _size(rng, 60000)
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    e, full = oracle.encode(k, p, data + [bytes(size)] * p)
+    assert e == 0
+    host = ia.host_alloc(n * size)
+    rows = [host[i * size:(i + 1) * size] for i in range(n)]
+    enc = ia.New(k, p)
+    op = str(rng.choice(["encode", "encode_verify", "verify", "reconstruct", "decode"]))
+    counts["pinned_" + op] += 1
+    tag = ("pinned", op, k, p, size)
+    for i in range(n):
+        rows[i][:] = full[i] if i < k or op in ("verify", "reconstruct", "decode") else 0x5C
+    if op in ("encode", "encode_verify"):
+        if op == "encode":
+            assert _call(enc, "rsgpu_encode", rows, [size] * n) == 0, tag
+        else:
+            ok = ctypes.c_int(0)
+            assert _call(enc, "rsgpu_encode_verify", rows, [size] * n, ctypes.byref(ok)) == 0, tag
+            assert ok.value == 1, tag
+        for r in range(k, n):
+            assert np.array_equal(rows[r], full[r]), tag
+    elif op == "verify":
+        if rng.random() < 0.5:
+            rows[int(rng.integers(0, n))][int(rng.integers(0, size))] ^= 0x11
+        e, want = oracle.verify(k, p, [r.copy() for r in rows])
+        ok = ctypes.c_int(7)
+        assert _call(enc, "rsgpu_verify", rows, [size] * n, ctypes.byref(ok)) == 0, tag
+        assert bool(ok.value) == want, tag
+    else:
+        lost = sorted(rng.choice(n, int(rng.integers(1, p + 1)), replace=False).tolist())
+        if rng.random() < 0.3:
+            rows[int(rng.integers(0, n))][int(rng.integers(0, size))] ^= 0x81
+        ref = [None if i in lost else rows[i].copy() for i in range(n)]
+        for i in lost:
+            rows[i][:] = 0xEE
+        lens = [0 if i in lost else size for i in range(n)]
+        e, want = oracle.reconstruct(k, p, ref)
+        assert e == 0
+        if op == "decode":
+            ok = ctypes.c_int(7)
+            assert _call(enc, "rsgpu_decode", rows, lens, ctypes.byref(ok)) == 0, tag
+            e2, want_ok = oracle.verify(k, p, want)
+            assert e2 == 0 and bool(ok.value) == want_ok, tag
+        else:
+            assert _call(enc, "rsgpu_reconstruct", rows, lens, 0) == 0, tag
+        for i in range(n):
+            assert np.array_equal(rows[i], want[i]), (tag, lost, i)
+
+
+def test_gpu_soak_vs_oracle(gpu):
+    seed = int(os.environ.get("RSGPU_SOAK_SEED", "20261016"))
+    rng = np.random.default_rng(seed)
+    counts = collections.Counter()
+    t0 = last = time.time()
+    while time.time() - t0 < SECONDS:
+        r = rng.random()
+        if r < 0.4:
+            _host_case(rng, counts)
+        elif r < 0.75:
+            _device_case(rng, counts)
+        else:
+            _pinned_case(rng, counts)
+        if time.time() - last > 30:  # progress line (a silent GPU run reads as hung)
+            last = time.time()
+            print(f"soak {last - t0:.0f}s: {sum(counts.values())} cases", flush=True)
+    print(f"soak seed {seed}, {time.time() - t0:.0f} s, {sum(counts.values())} cases:", flush=True)
+    for key in sorted(counts):
+        print(f"  {key:22s} {counts[key]}", flush=True)
