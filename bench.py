@@ -41,6 +41,15 @@ WORKLOADS = {
                          mixed=True,
                          desc="RS(10+2) encode+decode, 1 MiB objects, batch 1024/GPU, per-object "
                               "random erasure pair (mixed-pattern decode)"),
+    # small objects (4 KiB): rows of 26 vectors, packed 9 objects per
+    # workgroup; pitch = S rounded to 16 B (no padding traffic)
+    "small": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
+                  palign=16,
+                  desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, device-resident"),
+    "small_mixed": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
+                        palign=16, mixed=True,
+                        desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, per-object "
+                             "random erasure pair (mixed-pattern decode)"),
     "enc": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(), ops=("encode",),
                 desc="RS(10+2) encode, 1 MiB objects, batch 1024/GPU, device-resident"),
     # a healthy RS(10+4) Get receives exactly k = 10 bodies (proxy first-d
@@ -55,6 +64,8 @@ METRICS = {
     "encdec": "RS(10+2) encode+decode GiB/s (device-resident), 1 MB objects, 1/2/4/8 GPU",
     "encdec_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 1 MB objects",
     "enc": "RS(10+2) encode GiB/s (device-resident), 1 MB objects",
+    "small": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
+    "small_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 4 KiB objects",
     "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
 }
 
@@ -467,7 +478,8 @@ def main():
     if args.strong:
         nobj = shard_objects(nobj, rank, world)[1]
     S = (w["nbytes"] + k - 1) // k
-    pitch = (S + 255) // 256 * 256
+    pal = w.get("palign", 256)
+    pitch = (S + pal - 1) // pal * pal
     stride = n * pitch
     enc = ia.New(k, p, device=local)
     stream = torch.cuda.current_stream(dev)
@@ -491,8 +503,11 @@ def main():
     if w.get("mixed"):  # per-object random erasure pair (seeded)
         prs = np.random.default_rng(20200225 + rank)
         pres_m = np.ones((nobj, n), dtype=np.uint8)
-        for o in range(nobj):
-            pres_m[o, prs.choice(n, p, replace=False)] = 0
+        if nobj <= 4096:
+            for o in range(nobj):
+                pres_m[o, prs.choice(n, p, replace=False)] = 0
+        else:  # vectorised: the p smallest of n uniform keys per object
+            np.put_along_axis(pres_m, np.argsort(prs.random((nobj, n)), axis=1)[:, :p], 0, axis=1)
 
     turn = [0]
 

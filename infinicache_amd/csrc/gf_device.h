@@ -136,6 +136,10 @@ struct MultiArgs {  // per-object passes (a Get batch with mixed erasure pattern
     const Pass<K, R> *passes;  // device array, one per distinct pattern
     const uint32_t *objs;
     const uint32_t *obj_pass;  // ... with passes[obj_pass[i]]
+    // opw > 1 (small objects): item i is a group of opw objects sharing one
+    // pass, objs[i*opw + j] (~0u: empty slot), passes[obj_pass[i]]; lanes
+    // address object o at o * obj_stride from base, within gspan bytes
+    uint32_t opw, gspan;
 };
 
 // One workgroup = BS lanes x U vectors of 16 B of one object (grid.y).
@@ -284,6 +288,17 @@ __global__ __launch_bounds__(BS) void gf_apply_multi(const MultiArgs<K, R> m) {
     // index, pass index and the pass itself with s_load (invariant, uniform)
     uint32_t item, chunk;
     if (!wg_item(m.ord, item, chunk)) return;
+    if (m.opw > 1) {  // small objects: lane -> (object j of the group, vector v)
+        const __attribute__((address_space(4))) Pass<K, R> &p =
+            ((constant_ptr<Pass<K, R>>)m.passes)[((constant_ptr<uint32_t>)m.obj_pass)[item]];
+        const uint32_t j = threadIdx.x / m.nvec;
+        if (j >= m.opw) return;
+        const uint32_t obj = m.objs[item * m.opw + j];
+        if (obj == 0xffffffffu) return;
+        gf_apply_body<K, R, U, BS, LAUX, SAUX>(m.base, obj, p, m.nvec, m.tail, m.bad, threadIdx.x - j * m.nvec,
+                                               Redirect(), obj * (uint32_t)m.obj_stride, m.gspan);
+        return;
+    }
     const uint32_t obj = ((constant_ptr<uint32_t>)m.objs)[item];
     const uint32_t pi = ((constant_ptr<uint32_t>)m.obj_pass)[item];
     const __attribute__((address_space(4))) Pass<K, R> &p = ((constant_ptr<Pass<K, R>>)m.passes)[pi];

@@ -342,6 +342,51 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
         }
         nobj += es[i]->objs.size();
     }
+    bool stores = false;
+    for (const Entry *e : es) stores |= e->sub.nw > 0;
+    // Small objects (rows of <= half a workgroup's vectors): a workgroup codes
+    // opw objects of ONE pattern (sorted by pattern, address order within),
+    // lanes addressing object o at o * obj_stride from the batch base — so
+    // the batch must lie in one 32-bit buffer range.
+    uint32_t maxobj = 0;
+    for (const Entry *e : es)
+        for (uint32_t o : e->objs) maxobj = std::max(maxobj, o);
+    const size_t gspan = (size_t)maxobj * L.obj_stride + (size_t)L.pitch * 256;  // >= any pass span
+    if (kUnroll == 1 && nvec * 2 <= kBlock && gspan <= 0xffffffffull) {
+        const uint32_t opw = kBlock / nvec;
+        size_t ngroups = 0;
+        for (const Entry *e : es) ngroups += (e->objs.size() + opw - 1) / opw;
+        align();
+        const size_t objs_off = img.size();
+        img.resize(objs_off + ngroups * (opw + 1) * 4);
+        uint32_t *gobjs = (uint32_t *)&img[objs_off], *gpass = gobjs + ngroups * opw;
+        size_t g = 0;
+        for (size_t i = 0; i < es.size(); ++i) {
+            const std::vector<uint32_t> &os = es[i]->objs;  // ascending (launch_plans_multi)
+            for (size_t a = 0; a < os.size(); a += opw, ++g) {
+                for (uint32_t j = 0; j < opw; ++j) gobjs[g * opw + j] = a + j < os.size() ? os[a + j] : 0xffffffffu;
+                gpass[g] = (uint32_t)i;
+            }
+        }
+        return [=](const uint8_t *dimg, hipStream_t st) -> hipError_t {
+            MultiArgs<K, R> m;
+            m.base = L.base;
+            m.obj_stride = L.obj_stride;
+            m.bad = d_bad;
+            m.nvec = nvec;
+            m.tail = (uint32_t)(L.shard_len - (size_t)(nvec - 1) * 16);
+            m.passes = (const Pass<K, R> *)(dimg + pass_off);
+            m.objs = (const uint32_t *)(dimg + objs_off);
+            m.obj_pass = m.objs + ngroups * opw;
+            m.opw = opw;
+            m.gspan = (uint32_t)gspan;
+            unsigned grid;
+            m.ord = make_order(1, (uint32_t)ngroups, gspan, grid);
+            hipLaunchKernelGGL((gf_apply_multi<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kMultiChunks>),
+                               dim3(grid), dim3(kBlock), stores ? store_lds(K) : 0u, st, m);
+            return hipGetLastError();
+        };
+    }
     align();
     const size_t objs_off = img.size();
     img.resize(objs_off + nobj * 8);
@@ -358,10 +403,10 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
         objs[j] = items[j].first;
         pidx[j] = items[j].second;
     }
-    bool stores = false;
-    for (const Entry *e : es) stores |= e->sub.nw > 0;
     return [=](const uint8_t *dimg, hipStream_t st) -> hipError_t {
         MultiArgs<K, R> m;
+        m.opw = 1;
+        m.gspan = 0;
         m.base = L.base;
         m.obj_stride = L.obj_stride;
         m.bad = d_bad;
@@ -536,6 +581,7 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
     // entries grouped into (K, R) classes; K > 16 plans run object by object
     std::vector<std::vector<Entry>> per_plan(plans.size());
     std::vector<std::vector<uint32_t>> objs_of(plans.size());
+    // each plan's objects in ascending order (stage_class relies on it)
     for (size_t o = 0; o < plan_of.size(); ++o)
         if (plan_of[o] >= 0) objs_of[plan_of[o]].push_back((uint32_t)o);  // -1: skip object
     std::map<std::pair<int, int>, std::vector<const Entry *>> classes;

@@ -554,6 +554,55 @@ static int recon_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_
     return RSGPU_OK;
 }
 
+// Bitmask of the nonzero bytes of flags[0, n), n <= 64: eight flags per
+// word (OR-fold each byte onto its low bit, then gather the low bits).
+static uint64_t present_mask(const uint8_t *flags, int n) {
+    uint64_t mask = 0;
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, flags + i, 8);
+        w |= w >> 4;
+        w |= w >> 2;
+        w |= w >> 1;
+        w &= 0x0101010101010101ull;
+        mask |= ((w * 0x0102040810204080ull) >> 56) << i;
+    }
+    for (; i < n; ++i) mask |= (uint64_t)(flags[i] != 0) << i;
+    return mask;
+}
+
+// mask -> plan index (-1: not yet planned), open addressing, load <= 1/2
+struct PatternTable {
+    std::vector<uint64_t> keys;
+    std::vector<int> vals;
+    std::vector<uint8_t> used;
+    size_t count = 0;
+    PatternTable() : keys(256), vals(256), used(256) {}
+    static size_t hash(uint64_t k) { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> 32); }
+    int &find_or_insert(uint64_t k) {
+        if (2 * (count + 1) > keys.size()) grow();
+        size_t m = keys.size() - 1, h = hash(k) & m;
+        while (used[h] && keys[h] != k) h = (h + 1) & m;
+        if (!used[h]) {
+            used[h] = 1;
+            keys[h] = k;
+            vals[h] = -1;
+            ++count;
+        }
+        return vals[h];
+    }
+    void grow() {
+        PatternTable t;
+        t.keys.assign(keys.size() * 2, 0);
+        t.vals.assign(keys.size() * 2, 0);
+        t.used.assign(keys.size() * 2, 0);
+        for (size_t i = 0; i < keys.size(); ++i)
+            if (used[i]) t.find_or_insert(keys[i]) = vals[i];
+        *this = std::move(t);
+    }
+};
+
 // Mixed erasure patterns: present is nobj x (data+parity).  Objects are
 // grouped by pattern (one cached plan each) and coded by one launch per
 // (K, R) class (launch_plans_multi).
@@ -564,8 +613,11 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
     const int n = ctx->n;
-    // pattern key: the present bitmask (n <= 64: one word; else a byte string)
-    std::unordered_map<uint64_t, int> idx64;
+    // pattern key: the present bitmask (n <= 64: one word, looked up in an
+    // open-addressing table — a Get batch of 4 KiB objects holds 10^5+
+    // objects, and this loop is host time in front of the launch; else a
+    // byte string)
+    PatternTable idx64;
     std::map<std::string, int> idx_str;
     std::vector<std::shared_ptr<Plan>> owned;
     std::vector<Plan *> plans;
@@ -574,19 +626,19 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     for (int o = 0; o < nobj; ++o) {
         const uint8_t *pr = present + (size_t)o * n;
         uint64_t mask = 0;
-        int np = 0;
-        for (int i = 0; i < n; ++i) {
-            if (pr[i]) {
-                ++np;
-                if (i < 64) mask |= 1ull << i;
-            }
+        int np;
+        if (n <= 64) {
+            mask = present_mask(pr, n);
+            np = __builtin_popcountll(mask);
+        } else {
+            np = 0;
+            for (int i = 0; i < n; ++i) np += pr[i] != 0;
         }
         if (np < ctx->k) return RSGPU_ERR_TOO_FEW_SHARDS;
         if (np == n && !check) continue;  // nothing to reconstruct
         int *slot_idx;
         if (n <= 64) {
-            auto ins = idx64.emplace(mask, -1);
-            slot_idx = &ins.first->second;
+            slot_idx = &idx64.find_or_insert(mask);
         } else {
             std::string key(n, '0');
             for (int i = 0; i < n; ++i) key[i] = pr[i] ? '1' : '0';

@@ -555,12 +555,16 @@ def test_decode_batch_mixed_patterns(gpu):
 
 # ------------------------------------------------ mixed erasure patterns
 
-@pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 50001, 300), (10, 4, 7777, 120), (20, 4, 3000, 40)])
+@pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 50001, 300), (10, 4, 7777, 120), (20, 4, 3000, 40),
+                                        (10, 2, 103, 2000), (10, 4, 410, 700), (12, 4, 2048, 90),
+                                        (4, 2, 1, 300)])
 def test_dev_decode_multi_random_patterns(gpu, k, p, S, nobj):
     """A batch of Gets, each object with its own erasure pattern (0..p lost;
-    fewer lost than p leaves extra shards that are really checked)."""
+    fewer lost than p leaves extra shards that are really checked).  Shards
+    of <= 2 KiB take the packed small-object form (a workgroup codes several
+    objects of one pattern)."""
     n = k + p
-    pitch = (S + 255) // 256 * 256
+    pitch = (S + 255) // 256 * 256 if S >= 4096 else (S + 15) // 16 * 16
     stride = n * pitch
     rng = np.random.default_rng(k * 1000 + p)
     b = _dev_batch(nobj, n, S, pitch, seed=S + nobj)
@@ -578,7 +582,7 @@ def test_dev_decode_multi_random_patterns(gpu, k, p, S, nobj):
         if nl < p and o % 7 == 0:  # an extra present shard exists: corrupt the last present row
             last = int(np.nonzero(present[o])[0][-1])
             if last >= k:  # upstream Verify checks parity rows only
-                b[o, last, 3] ^= 1
+                b[o, last, min(3, S - 1)] ^= 1
                 corrupt.add(o)
     bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
     enc.decode_dev_multi(b, present, S, pitch, stride, nobj, bad, s)
