@@ -572,13 +572,20 @@ static uint64_t present_mask(const uint8_t *flags, int n) {
     return mask;
 }
 
-// mask -> plan index (-1: not yet planned), open addressing, load <= 1/2
+// mask -> plan index (-1: not yet planned): a direct table for n <= 16
+// shards, else open addressing with load <= 1/2
 struct PatternTable {
+    explicit PatternTable(int n) : direct(n <= 16 ? (size_t)1 << n : 0, -1) {
+        if (direct.empty()) keys.resize(256), vals.resize(256), used.resize(256);
+    }
+    int &operator[](uint64_t k) { return direct.empty() ? find_or_insert(k) : direct[k]; }
+
+  private:
+    std::vector<int> direct;
     std::vector<uint64_t> keys;
     std::vector<int> vals;
     std::vector<uint8_t> used;
     size_t count = 0;
-    PatternTable() : keys(256), vals(256), used(256) {}
     static size_t hash(uint64_t k) { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> 32); }
     int &find_or_insert(uint64_t k) {
         if (2 * (count + 1) > keys.size()) grow();
@@ -593,13 +600,15 @@ struct PatternTable {
         return vals[h];
     }
     void grow() {
-        PatternTable t;
-        t.keys.assign(keys.size() * 2, 0);
-        t.vals.assign(keys.size() * 2, 0);
-        t.used.assign(keys.size() * 2, 0);
-        for (size_t i = 0; i < keys.size(); ++i)
-            if (used[i]) t.find_or_insert(keys[i]) = vals[i];
-        *this = std::move(t);
+        std::vector<uint64_t> k2(keys.size() * 2);
+        std::vector<int> v2(keys.size() * 2);
+        std::vector<uint8_t> u2(keys.size() * 2);
+        std::swap(k2, keys);
+        std::swap(v2, vals);
+        std::swap(u2, used);
+        count = 0;
+        for (size_t i = 0; i < k2.size(); ++i)
+            if (u2[i]) find_or_insert(k2[i]) = v2[i];
     }
 };
 
@@ -613,11 +622,10 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
     const int n = ctx->n;
-    // pattern key: the present bitmask (n <= 64: one word, looked up in an
-    // open-addressing table — a Get batch of 4 KiB objects holds 10^5+
-    // objects, and this loop is host time in front of the launch; else a
-    // byte string)
-    PatternTable idx64;
+    // pattern key: the present bitmask (n <= 64: one word, looked up in a
+    // PatternTable — a Get batch of 4 KiB objects holds 10^5+ objects, and
+    // this loop is host time in front of the launch; else a byte string)
+    PatternTable idx64(n);
     std::map<std::string, int> idx_str;
     std::vector<std::shared_ptr<Plan>> owned;
     std::vector<Plan *> plans;
@@ -638,7 +646,7 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
         if (np == n && !check) continue;  // nothing to reconstruct
         int *slot_idx;
         if (n <= 64) {
-            slot_idx = &idx64.find_or_insert(mask);
+            slot_idx = &idx64[mask];
         } else {
             std::string key(n, '0');
             for (int i = 0; i < n; ++i) key[i] = pr[i] ? '1' : '0';
