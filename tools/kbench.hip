@@ -575,6 +575,78 @@ std::vector<Variant> small_variants() {
     };
 }
 
+// KB_SET=burst: store bursts.  A workgroup codes CH consecutive 4 KiB chunks
+// of one object, holding all outputs in VGPRs, then stores them: each output
+// row gets CH*4 KiB in one burst per workgroup (the write stream arrives in
+// larger runs).  Shapes with nw == R only (encode, decode without checks).
+template <int K, int R, int CH>
+__global__ __launch_bounds__(256) void apply_burst(const ApplyArgs<K, R> a) {
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)obj * a.obj_stride), (short)0, (int)a.p.span, 0x00020000);
+    u32x4 out[CH][R];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const uint32_t v = (chunk * CH + ch) * 256u + threadIdx.x;
+        u32x4 x[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.p.in_off[c], 2);
+        uint32_t acc[R][4];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const GfIdx g = gf_idx(x[c][d]);
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], &a.p.tab[(c * R + r) * kTabWords], g);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) out[ch][r] = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int ch = 0; ch < CH; ++ch) {
+            const uint32_t v = (chunk * CH + ch) * 256u + threadIdx.x;
+            if (v < a.nvec) __builtin_amdgcn_raw_buffer_store_b128(out[ch][r], rs, v * 16u, a.p.out_off[r], 2);
+        }
+    if (a.p.clear && chunk == 0 && threadIdx.x == 0) a.bad[obj] = 0u;
+}
+template <int K, int R, int CH, int W>
+void launch_burst(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    grid.x = (grid.x + CH - 1) / CH;
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    const int w = W > 0 ? W : (K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K));
+    hipLaunchKernelGGL((apply_burst<K, R, CH>), dim3(nb), dim3(256), W < 0 ? 0u : 160u * 1024u / (unsigned)w - 256u,
+                       st, a);
+}
+template <int K, int R>
+std::vector<Variant> burst_variants() {
+    return {
+        {"shipped", launch_ship<K, R>, 1, 256, false},
+        {"burst CH1, lib cap", launch_burst<K, R, 1, 0>, 1, 256, false},
+        {"burst CH2, lib cap", launch_burst<K, R, 2, 0>, 1, 256, false},
+        {"burst CH4, lib cap", launch_burst<K, R, 4, 0>, 1, 256, false},
+        {"burst CH2, cap 8", launch_burst<K, R, 2, 8>, 1, 256, false},
+        {"burst CH4, cap 8", launch_burst<K, R, 4, 8>, 1, 256, false},
+        {"burst CH4, full occupancy", launch_burst<K, R, 4, -1>, 1, 256, false},
+        {"burst CH8, full occupancy", launch_burst<K, R, 8, -1>, 1, 256, false},
+    };
+}
+
 // KB_SET=multi: cost of the mixed-pattern kernel's per-workgroup lookups
 // (object index, pass index, then the pass) on a uniform pattern, and its
 // occupancy cap
@@ -803,6 +875,7 @@ std::vector<Variant> variants() {
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "stream") return stream_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "rows") return rows_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "multi") return multi_variants<K, R>();
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "burst") return burst_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "small") return small_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "occ") return occ_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "capp") return capp_variants<K, R>();
