@@ -17,7 +17,10 @@
 //   * rows [0, nw) are stored with buffer_store_dwordx4; rows [nw, R) are
 //     compare-to-zero rows that raise a per-object flag (fused Verify);
 //   * non-temporal loads and stores, and on passes that store rows an
-//     occupancy cap through an LDS reservation (store_lds below).
+//     occupancy cap through an LDS reservation (store_lds below);
+//   * short rows (<= 128 vectors): one workgroup codes 256 / nvec whole
+//     objects, lane -> (object, vector) (launch_fixed; the mixed-pattern
+//     kernel groups same-pattern objects the same way, stage_class).
 // No MFMA and no LDS data: the op is HBM-bound byte arithmetic.
 #include <hip/hip_runtime.h>
 
