@@ -130,3 +130,38 @@ def test_device_layout_validation():
         enc.encode_dev(4096, 100, 112, 112, 2)           # objects overlap
     with pytest.raises(ia.ErrShardNoData):
         enc.encode_dev(4096, 0, 112, 12 * 112, 1)
+
+
+@pytest.mark.parametrize("k,p", [(10, 2), (10, 4), (6, 3), (40, 20), (200, 50)])
+def test_mixed_pattern_planning_without_device(k, p):
+    """rsgpu_decode_dev_multi plans every object's pattern on the host before
+    touching a device (present mask built eight flags per word, direct table
+    for n <= 16 shards, open addressing up to 64, byte strings beyond): an
+    object with fewer than k present shards is ErrTooFewShards wherever it
+    sits in the batch and whatever nonzero values mark present flags; a valid
+    batch gets as far as the device (ErrNoDevice here, on a CPU box)."""
+    L = _lib.load()
+    n = k + p
+    enc = ia.New(k, p)
+    rng = np.random.default_rng(n)
+    nobj = 3000 if n <= 16 else 1000 if n <= 64 else 40  # distinct patterns cost one inverse each
+    pm = np.ones((nobj, n), dtype=np.uint8)
+    for o in range(nobj):  # lose 0..p shards, present flags any nonzero byte
+        pm[o, rng.choice(n, int(rng.integers(0, p + 1)), replace=False)] = 0
+        pm[o] *= rng.integers(1, 256, n, dtype=np.uint8)
+    base = ctypes.c_void_p(1 << 20)  # never dereferenced: planning fails first or no device
+    bad = ctypes.c_void_p(1 << 21)
+
+    def call(m):
+        m = np.ascontiguousarray(m)
+        return L.rsgpu_decode_dev_multi(enc._ctx, base, m.ctypes.data_as(_lib.u8p), 64, 64, n * 64,
+                                        nobj, bad, None)
+
+    if not ia.device_ok(0):
+        no_device = int(re.search(r"#define RSGPU_ERR_NO_DEVICE (-?\d+)", open(_lib.HEADER).read()).group(1))
+        assert call(pm) == no_device
+    for where in sorted({0, 7, 8, nobj // 2, nobj - 1}):
+        m = pm.copy()
+        m[where, :] = 0
+        m[where, rng.choice(n, k - 1, replace=False)] = 0x80  # k-1 present
+        assert call(m) == oracle.ERR_TOO_FEW_SHARDS, where
