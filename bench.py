@@ -50,6 +50,12 @@ WORKLOADS = {
                         palign=16, mixed=True,
                         desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, per-object "
                              "random erasure pair (mixed-pattern decode)"),
+    # upstream Get semantics, unfused (reported separately, not
+    # the headline): Reconstruct, then a full Verify pass over all k+p rows
+    "encdec_upstream": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(0, 5), ops=("encode", "decode"),
+                            upstream_get=True,
+                            desc="RS(10+2) encode+decode, 1 MiB objects, batch 1024/GPU, decode as upstream "
+                                 "Client.decode: Reconstruct then a separate full Verify pass"),
     "enc": dict(k=10, p=2, nbytes=1 << 20, batch=1024, lost=(), ops=("encode",),
                 desc="RS(10+2) encode, 1 MiB objects, batch 1024/GPU, device-resident"),
     # a healthy RS(10+4) Get receives exactly k = 10 bodies (proxy first-d
@@ -64,6 +70,7 @@ METRICS = {
     "encdec": "RS(10+2) encode+decode GiB/s (device-resident), 1 MB objects, 1/2/4/8 GPU",
     "encdec_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 1 MB objects",
     "enc": "RS(10+2) encode GiB/s (device-resident), 1 MB objects",
+    "encdec_upstream": "RS(10+2) encode+decode GiB/s (device-resident, unfused Reconstruct+Verify Get), 1 MB objects",
     "small": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
     "small_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 4 KiB objects",
     "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
@@ -521,7 +528,10 @@ def main():
         if evs is not None:
             evs[1].record(stream)
         if "decode" in w["ops"]:
-            if w.get("mixed"):
+            if w.get("upstream_get"):
+                enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=False, stream=stream)
+                enc.verify_dev(buf, S, pitch, stride, nobj, bad, stream)
+            elif w.get("mixed"):
                 enc.decode_dev_multi(buf, pres_m, S, pitch, stride, nobj, bad, stream)
             elif w.get("data_only"):
                 enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=True,
@@ -570,12 +580,16 @@ def main():
     e_rows = len(w["lost"])
     enc_bytes = nobj * (k + p) * S
     dec_bytes = nobj * (k + e_rows) * S
+    if w.get("upstream_get"):  # + Verify: reads all k+p rows again
+        dec_bytes += nobj * (k + p) * S
     # launches grouped by kernel symbol: encode and the uniform-pattern decode
     # of RS(10+2) are the same kernel (gf_apply_kernel<10,2>) with the same
     # algorithmic bytes per launch, so its average duration is over both, as
     # rocprofv3 --stats reports it
     enc_sym = f"gf_apply_kernel<{k},{p}>"
     dec_sym = f"gf_apply_{'multi' if w.get('mixed') else 'kernel'}<{k},{e_rows}>"
+    if w.get("upstream_get"):
+        dec_sym = f"gf_apply_kernel<{k},{e_rows}>+gf_apply_kernel<{k + p},{p}>"
     per_op = {}
     if "encode" in w["ops"]:
         per_op["encode"] = (enc_sym, enc_bytes, enc_ms)
