@@ -165,6 +165,26 @@ int rsgpu_reconstruct_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *pre
 int rsgpu_decode_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                            size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream);
 
+/* Mixed erasure patterns with the arrival bitmaps already in HBM:
+ * d_masks[o] (device, uint32) has bit i set when shard i of object o arrived
+ * (bits >= data+parity ignored).  The pattern -> coefficient resolution runs
+ * on the device against a per-context atlas of every erasure pattern, built
+ * and uploaded on the first call: no per-call host planning, upload or host
+ * synchronisation.  Requires data+parity <= 16 (else RSGPU_ERR_NOT_IMPLEMENTED;
+ * the host-flag *_dev_multi calls cover wider codes).
+ * d_status[o] (device uint32; optional for reconstruct) receives, per object:
+ *   0  done (decode: upstream's Verify-after-Reconstruct would pass),
+ *   1  decode only: that Verify would fail (ecRedis.go:420-426),
+ *   2  fewer than data shards present (upstream ErrTooFewShards): untouched,
+ *   3  survivors' matrix singular (upstream errSingular; non-MDS matrices): untouched.
+ * Same per-object semantics as rsgpu_decode_dev / rsgpu_reconstruct_dev
+ * (survivors = first data present shards in index order, as upstream). */
+int rsgpu_decode_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len,
+                           size_t pitch, size_t obj_stride, int nobj, uint32_t *d_status, void *stream);
+int rsgpu_reconstruct_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len,
+                                size_t pitch, size_t obj_stride, int nobj, int data_only,
+                                uint32_t *d_status, void *stream);
+
 /* ---- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
  * The path starts and ends in host memory (ecRedis.go:96 Set buffer,
  * ecRedis.go:161-170 gathered Get buffers).  These calls stream a batch of

@@ -22,7 +22,7 @@ EXPORTS = (
     "rsgpu_reconstruct_dev", "rsgpu_decode_dev", "rsgpu_reconstruct_dev_multi",
     "rsgpu_decode_dev_multi", "rsgpu_encode_batch", "rsgpu_decode_batch",
     "rsgpu_host_register", "rsgpu_host_unregister", "rsgpu_host_alloc", "rsgpu_host_free",
-    "rsgpu_encode_verify",
+    "rsgpu_encode_verify", "rsgpu_decode_dev_masks", "rsgpu_reconstruct_dev_masks",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -82,6 +82,8 @@ def load():
     L.rsgpu_decode_dev.argtypes = [vp, vp, u8p, sz, sz, sz, ci, vp, vp]
     L.rsgpu_reconstruct_dev_multi.argtypes = [vp, vp, u8p, sz, sz, sz, ci, ci, vp]
     L.rsgpu_decode_dev_multi.argtypes = [vp, vp, u8p, sz, sz, sz, ci, vp, vp]
+    L.rsgpu_decode_dev_masks.argtypes = [vp, vp, vp, sz, sz, sz, ci, vp, vp]
+    L.rsgpu_reconstruct_dev_masks.argtypes = [vp, vp, vp, sz, sz, sz, ci, ci, vp, vp]
     L.rsgpu_encode_batch.argtypes = [vp, u8pp, szp, ci]
     L.rsgpu_decode_batch.argtypes = [vp, u8pp, u8p, szp, ci, intp]
     L.rsgpu_host_register.argtypes = [vp, sz]

@@ -80,6 +80,26 @@ struct Pipeline {
     }
 };
 
+// Device atlas of every erasure pattern of one operation (gf_masked.h),
+// built and uploaded on the first *_dev_masks call, then immutable.
+struct Atlas {
+    std::once_flag host_once, dev_once;  // host build (no device needed), then upload
+    int host_err = 0, dev_err = 0;
+    int32_t *d_pat = nullptr;
+    void *d_recs = nullptr;
+    uint32_t *d_tabs = nullptr;
+    std::vector<int32_t> h_pat;   // pattern table, kept (host-flag calls validate with it)
+    std::vector<uint8_t> h_recs;  // PatRec image, freed after the upload
+    std::vector<uint32_t> h_tabs; // kernel tables, freed after the upload
+    AtlasView view;
+    ~Atlas() {
+        if (d_pat) (void)hipFree(d_pat);
+        if (d_recs) (void)hipFree(d_recs);
+        if (d_tabs) (void)hipFree(d_tabs);
+    }
+};
+enum AtlasMode { kAtlasReconstruct = 0, kAtlasData = 1, kAtlasDecode = 2 };
+
 }  // namespace rsgpu
 
 using namespace rsgpu;
@@ -87,6 +107,14 @@ using namespace rsgpu;
 struct rsgpu_ctx {
     rsgpu::Pipeline pipe;  // batch host API (pipeline.cpp)
     rsgpu::MultiWorkspace multi_ws;  // mixed-pattern device launches
+    rsgpu::Atlas atlas[3];           // device-resolved patterns, per AtlasMode
+    uint32_t *d_ctab = nullptr;      // [256][8] coefficient tables (gf_apply_lanes)
+    std::once_flag ctab_once;
+    int ctab_err = 0;
+    rsgpu::StatusScratch scratch;    // multi-reporter status of the masked decode
+    ~rsgpu_ctx() {
+        if (d_ctab) (void)hipFree(d_ctab);
+    }
     int k = 0, p = 0, n = 0;
     unsigned kind = 0;
     int device = 0;
@@ -164,12 +192,7 @@ struct rsgpu_ctx {
     std::shared_ptr<Plan> plan_verify() {
         if (auto p = cached("V")) return p;
         auto p = std::make_shared<Plan>();
-        p->K = n; p->R = this->p; p->nw = 0;
-        for (int c = 0; c < n; ++c) p->in_rows.push_back(c);
-        for (int j = k; j < n; ++j) {
-            p->out_rows.push_back(-1);
-            for (int c = 0; c < n; ++c) p->coef.push_back(c < k ? row(j)[c] : (uint8_t)(c == j));
-        }
+        build_verify(*p);
         return remember("V", p);
     }
 
@@ -212,6 +235,17 @@ struct rsgpu_ctx {
         std::string key = check ? "D" : (data_only ? "d" : "R");
         for (int i = 0; i < n; ++i) key.push_back(present[i] ? '1' : '0');
         if ((out = cached(key))) return RSGPU_OK;
+        auto p = std::make_shared<Plan>();
+        int e = build_reconstruct(present, data_only, check, *p);
+        if (e) return e;
+        out = remember(key, p);
+        return RSGPU_OK;
+    }
+
+    // The plan of one erasure pattern (no caching of the plan itself; the
+    // survivors' inverse goes through the inverse cache).  Tables not built.
+    int build_reconstruct(const uint8_t *present, bool data_only, bool check, Plan &pl) {
+        Plan *p = &pl;
         std::vector<int> surv, extra, miss;
         for (int i = 0; i < n; ++i) {
             if (present[i]) (surv.size() < (size_t)k ? surv : extra).push_back(i);
@@ -221,7 +255,6 @@ struct rsgpu_ctx {
         int e = inverse(surv, inv);
         if (e) return e;
         const GF &g = gf();
-        auto p = std::make_shared<Plan>();
         p->in_rows = surv;
         if (check) p->in_rows.insert(p->in_rows.end(), extra.begin(), extra.end());
         p->K = (int)p->in_rows.size();
@@ -257,9 +290,25 @@ struct rsgpu_ctx {
             }
         }
         p->R = (int)p->out_rows.size();
-        out = remember(key, p);
         return RSGPU_OK;
     }
+
+    // Verify's plan: check rows M[j] x data XOR parity_j (j in [k, n)),
+    // tables not built
+    void build_verify(Plan &p) {
+        p.K = n; p.R = this->p; p.nw = 0;
+        p.in_rows.clear(); p.out_rows.clear(); p.coef.clear();
+        for (int c = 0; c < n; ++c) p.in_rows.push_back(c);
+        for (int j = k; j < n; ++j) {
+            p.out_rows.push_back(-1);
+            for (int c = 0; c < n; ++c) p.coef.push_back(c < k ? row(j)[c] : (uint8_t)(c == j));
+        }
+    }
+
+    // rsgpu.cpp: the atlas's host part (pattern table; no device needed), and
+    // the uploaded atlas the kernels read
+    int atlas_host(AtlasMode mode, const Atlas *&out);
+    int atlas_view(AtlasMode mode, AtlasView &out);
 
     // ---- staging slots
     int get_slot(size_t bytes, std::unique_ptr<Slot> &s) {

@@ -11,6 +11,7 @@
 // (upstream buildMatrix / cached inverses); the kernel never branches on the
 // operation.
 #pragma once
+#include <array>
 #include <cstddef>
 #include <cstdint>
 #include <mutex>
@@ -43,10 +44,12 @@ struct Plan {
     uint32_t *d_in_row = nullptr;  // [K]
     std::once_flag dev_once;
     hipError_t dev_err = hipSuccess;
-    // serialized Pass images for mixed-pattern launches, per (pitch, first row)
+    // serialized Pass images for mixed-pattern launches, keyed by (pitch and
+    // flags, first row, vectors per row): the image's span depends on all three
     std::mutex img_mu;
-    std::vector<std::pair<std::pair<size_t, int>, std::vector<uint8_t>>> pass_imgs;
+    std::vector<std::pair<std::array<uint64_t, 3>, std::vector<uint8_t>>> pass_imgs;
     void build_tables();
+    int identity_inputs() const;  // trailing identity inputs (ki) of coef
     ~Plan();
 };
 
@@ -81,7 +84,29 @@ struct MultiWorkspace {
     // images go up on their own stream so the copy overlaps whatever the
     // caller's stream is still running (e.g. the previous kernel)
     hipStream_t upload = nullptr;
+    hipEvent_t uploaded[kRing] = {};  // GPU-side ordering of an upload before its kernels
+    std::vector<uint32_t> masks;      // host-flag calls: packed present masks
     ~MultiWorkspace();
+};
+
+// Zeroed scratch (acc, cnt: nobj u32 each) for launch_masked's multi-
+// reporter status, a ring so calls in flight on different streams never
+// share one.  The kernels leave it zero.
+struct StatusScratch {
+    static constexpr int kRing = 4;
+    struct Slot {
+        uint32_t *d = nullptr;  // [2][cap]
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+    };
+    std::mutex mu;
+    Slot slot[kRing];
+    unsigned next = 0;
+    // takes the next slot (waiting for the calls that used it), grows and
+    // zeroes it on `stream` when needed; release() records its completion
+    hipError_t acquire(size_t nobj, hipStream_t stream, Slot *&s);
+    hipError_t release(Slot *s, hipStream_t stream, bool ok);
+    ~StatusScratch();
 };
 
 // Object o of the layout is coded with plans[plan_of[o]] (a batch of Gets
@@ -96,5 +121,29 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
 // zeroed by the caller when the plan has check rows.  Returns hipSuccess or
 // the first HIP error.
 hipError_t launch_plan(Plan &plan, const Layout &L, uint32_t *d_bad, hipStream_t stream);
+
+// Device atlas of every erasure pattern of one operation (gf_masked.h): the
+// pattern table over all 2^n present masks, one record per (pattern,
+// sub-pass), the records' kernel tables, and the 256-entry coefficient table.
+struct AtlasView {
+    const int32_t *pat = nullptr;
+    const void *recs = nullptr;     // PatRec [slot][nsub]
+    const uint32_t *tabs = nullptr; // [slot][nsub][kmax][R][kCoefWords]
+    const uint32_t *ctab = nullptr; // [256][8]
+    int n = 0;      // shards: masks use bits [0, n)
+    int kmax = 0;   // inputs of the widest pattern (decode: n; reconstruct: k)
+    int R = 0;      // rows per sub-pass (<= 4)
+    int nsub = 0;   // sub-passes
+    int kfix = 0;   // inputs when every pattern has the same count (reconstruct: k), else 0
+    int kcap = 0;   // inputs of the common pattern (occupancy cap: a healthy Get has k)
+};
+
+// Codes every object of the layout with the pattern its device-resident
+// present mask selects (rsgpu_*_dev_masks).  status (nullable) receives
+// kStatus* per object; acc/cnt (nobj u32 each, all zero, left zero) are needed
+// when the atlas has check rows.  nvec <= 128 rows use gf_apply_lanes, longer
+// rows gf_apply_masked.
+hipError_t launch_masked(const AtlasView &A, const Layout &L, const uint32_t *d_masks, uint32_t *d_status,
+                         uint32_t *acc, uint32_t *cnt, hipStream_t stream);
 
 }  // namespace rsgpu

@@ -31,6 +31,7 @@
 #include "../../include/rsgpu.h"
 #include "gf256.h"
 #include "gf_apply.h"
+#include "gf_masked.h"
 
 namespace rsgpu {
 
@@ -275,6 +276,122 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     return RSGPU_OK;
 }
 
+// ------------------------------------------------- device pattern atlas
+// Every erasure pattern of the code, for one operation, as the device kernels
+// of gf_masked.h read it: the pattern table over all 2^n present masks, one
+// PatRec per (pattern, sub-pass) and its [kmax][R] kernel tables.  Built once
+// per context and mode (upstream's inversionTree holds the same inverses,
+// filled lazily), uploaded, then immutable.
+int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
+    const int n = ctx->n, k = ctx->k;
+    const bool check = mode == kAtlasDecode, data_only = mode == kAtlasData;
+    const size_t nm = (size_t)1 << n;
+    struct Ent {
+        int K, R, nw, ki;
+        std::vector<uint8_t> coef;
+        std::vector<int> out_rows;
+    };
+    std::vector<int32_t> pat(nm);
+    std::vector<Ent> ents;
+    std::vector<uint8_t> present(n);
+    int maxR = 0;
+    for (size_t mask = 0; mask < nm; ++mask) {
+        const int np = __builtin_popcountll(mask);
+        if (np < k) {
+            pat[mask] = kPatTooFew;
+            continue;
+        }
+        for (int i = 0; i < n; ++i) present[i] = (mask >> i) & 1;
+        Plan pl;
+        if (np == n) {
+            if (!check) {  // Reconstruct with every shard present: nothing to do
+                pat[mask] = kPatNothing;
+                continue;
+            }
+            ctx->build_verify(pl);  // Client.decode's first Verify
+        } else {
+            const int e = ctx->build_reconstruct(present.data(), data_only, check, pl);
+            if (e == RSGPU_ERR_SINGULAR) {
+                pat[mask] = kPatSingular;
+                continue;
+            }
+            if (e) return e;
+        }
+        if (pl.R == 0) {  // ReconstructData with only parity missing
+            pat[mask] = kPatNothing;
+            continue;
+        }
+        pat[mask] = (int32_t)ents.size();
+        ents.push_back({pl.K, pl.R, pl.nw, pl.identity_inputs(), pl.coef, pl.out_rows});
+        maxR = std::max(maxR, pl.R);
+    }
+    const int R = std::max(1, std::min(4, maxR)), nsub = std::max(1, (maxR + 3) / 4);
+    const int kmax = check ? n : k;
+    const size_t nrec = ents.size() * (size_t)nsub, tw = (size_t)kmax * R * kCoefWords;
+    if (nrec * tw * 4 > ((size_t)256 << 20)) return RSGPU_ERR_NOT_IMPLEMENTED;  // bound the atlas
+    std::vector<uint32_t> ct(256 * kCoefWords);
+    for (int c = 0; c < 256; ++c) coef_tables((uint8_t)c, &ct[(size_t)c * kCoefWords]);
+    std::vector<PatRec> recs(std::max<size_t>(nrec, 1));
+    std::memset(recs.data(), 0, recs.size() * sizeof(PatRec));
+    std::vector<uint32_t> tabs(std::max<size_t>(nrec * tw, 1), 0);
+    for (size_t i = 0; i < ents.size(); ++i) {
+        const Ent &e = ents[i];
+        int nchk = 0;
+        for (int s = 0; s < nsub; ++s) {
+            const int nr = std::max(0, std::min(4, e.R - 4 * s)), nw = std::max(0, std::min(nr, e.nw - 4 * s));
+            nchk += nw < nr;
+        }
+        for (int s = 0; s < nsub; ++s) {
+            const int r0 = 4 * s;
+            const int nr = std::max(0, std::min(4, e.R - r0)), nw = std::max(0, std::min(nr, e.nw - r0));
+            PatRec &rc = recs[i * nsub + s];
+            rc.kact = (uint8_t)e.K;
+            rc.nr = (uint8_t)nr;
+            rc.nw = (uint8_t)nw;
+            // identity inputs feed the plan's last rows: usable in its last sub-pass
+            rc.ki = (uint8_t)(nr > 0 && r0 + nr == e.R ? std::min(e.ki, nr) : 0);
+            rc.nchk = (uint8_t)nchk;
+            uint32_t *tb = &tabs[(i * nsub + s) * tw];
+            for (int r = 0; r < nr; ++r) {
+                if (r < nw) rc.out_row[r] = (uint8_t)e.out_rows[r0 + r];
+                for (int c = 0; c < e.K; ++c) {
+                    const uint8_t cf = e.coef[(size_t)(r0 + r) * e.K + c];
+                    rc.coef[r][c] = cf;
+                    std::memcpy(&tb[((size_t)c * R + r) * kCoefWords], &ct[(size_t)cf * kCoefWords], kCoefWords * 4);
+                }
+            }
+        }
+    }
+    A.h_pat = std::move(pat);
+    A.h_recs.resize(recs.size() * sizeof(PatRec));
+    std::memcpy(A.h_recs.data(), recs.data(), A.h_recs.size());
+    A.h_tabs = std::move(tabs);
+    AtlasView &v = A.view;
+    v.n = n;
+    v.kmax = kmax;
+    v.R = R;
+    v.nsub = nsub;
+    v.kfix = check ? 0 : k;
+    v.kcap = k;
+    return RSGPU_OK;
+}
+
+int upload_atlas(rsgpu_ctx *ctx, Atlas &A) {
+    HIP_TRY(hipMalloc(&A.d_pat, A.h_pat.size() * 4));
+    HIP_TRY(hipMemcpy(A.d_pat, A.h_pat.data(), A.h_pat.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&A.d_recs, A.h_recs.size()));
+    HIP_TRY(hipMemcpy(A.d_recs, A.h_recs.data(), A.h_recs.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&A.d_tabs, A.h_tabs.size() * 4));
+    HIP_TRY(hipMemcpy(A.d_tabs, A.h_tabs.data(), A.h_tabs.size() * 4, hipMemcpyHostToDevice));
+    std::vector<uint8_t>().swap(A.h_recs);
+    std::vector<uint32_t>().swap(A.h_tabs);
+    A.view.pat = A.d_pat;
+    A.view.recs = A.d_recs;
+    A.view.tabs = A.d_tabs;
+    A.view.ctab = ctx->d_ctab;
+    return RSGPU_OK;
+}
+
 int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_t pitch,
                  size_t obj_stride, int nobj) {
     if (!base || nobj < 0) return RSGPU_ERR_INVALID_ARG;
@@ -284,6 +401,67 @@ int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_
     if ((size_t)ctx->n * pitch >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
     if (nobj > 1 && obj_stride < (size_t)ctx->n * pitch) return RSGPU_ERR_INVALID_ARG;
     return RSGPU_OK;
+}
+
+}  // namespace
+
+int rsgpu_ctx::atlas_host(AtlasMode mode, const Atlas *&out) {
+    if (n > kAtlasMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
+    Atlas &A = atlas[mode];
+    std::call_once(A.host_once, [&] { A.host_err = build_atlas_host(this, mode, A); });
+    out = &A;
+    return A.host_err;
+}
+
+int rsgpu_ctx::atlas_view(AtlasMode mode, AtlasView &out) {
+    const Atlas *ah;
+    int e = atlas_host(mode, ah);
+    if (e) return e;
+    std::call_once(ctab_once, [&] {
+        std::vector<uint32_t> t(256 * kCtabStride, 0);
+        for (int c = 0; c < 256; ++c) coef_tables((uint8_t)c, &t[(size_t)c * kCtabStride]);
+        hipError_t e = hipMalloc(&d_ctab, t.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(d_ctab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+        ctab_err = e == hipSuccess ? RSGPU_OK : hip_fail(e, "atlas coefficient table");
+    });
+    if (ctab_err) return ctab_err;
+    Atlas &A = atlas[mode];
+    std::call_once(A.dev_once, [&] { A.dev_err = upload_atlas(this, A); });
+    if (A.dev_err) return A.dev_err;
+    out = A.view;
+    return RSGPU_OK;
+}
+
+namespace {
+
+// launch_masked with the multi-reporter status scratch the decode needs
+int run_masked(rsgpu_ctx *ctx, const AtlasView &A, AtlasMode mode, const Layout &L, const uint32_t *d_masks,
+               uint32_t *d_status, hipStream_t st) {
+    if (mode != kAtlasDecode) {
+        HIP_TRY(launch_masked(A, L, d_masks, d_status, nullptr, nullptr, st));
+        return RSGPU_OK;
+    }
+    StatusScratch::Slot *sc = nullptr;
+    HIP_TRY(ctx->scratch.acquire((size_t)L.nobj, st, sc));
+    const hipError_t e = launch_masked(A, L, d_masks, d_status, sc->d, sc->d + sc->cap, st);
+    const hipError_t e2 = ctx->scratch.release(sc, st, e == hipSuccess);
+    if (e != hipSuccess) return hip_fail(e, "launch_masked");
+    if (e2 != hipSuccess) return hip_fail(e2, "status scratch");
+    return RSGPU_OK;
+}
+
+int dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len, size_t pitch,
+              size_t obj_stride, int nobj, AtlasMode mode, uint32_t *d_status, void *stream) {
+    if (!ctx || (nobj > 0 && !d_masks)) return RSGPU_ERR_INVALID_ARG;
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    if (e) return e;
+    if (ctx->n > kAtlasMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
+    if ((e = ctx->use_device())) return e;
+    if (nobj == 0) return RSGPU_OK;
+    AtlasView A;
+    if ((e = ctx->atlas_view(mode, A))) return e;
+    Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
+    return run_masked(ctx, A, mode, L, d_masks, d_status, (hipStream_t)stream);
 }
 
 }  // namespace
@@ -615,6 +793,63 @@ struct PatternTable {
 // Mixed erasure patterns: present is nobj x (data+parity).  Objects are
 // grouped by pattern (one cached plan each) and coded by one launch per
 // (K, R) class (launch_plans_multi).
+// Host present flags -> masks, uploaded from a pinned ring slot on a side
+// stream (no host wait), then the device-resolved passes (n <= 16).  Argument
+// errors (too few shards, a singular pattern) are returned before any launch.
+static int recon_dev_multi_atlas(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
+                                 size_t pitch, size_t obj_stride, int nobj, AtlasMode mode,
+                                 uint32_t *d_bad, void *stream) {
+    const int n = ctx->n;
+    const Atlas *ah;
+    int e = ctx->atlas_host(mode, ah);
+    if (e) return e;
+    MultiWorkspace &ws = ctx->multi_ws;
+    std::lock_guard<std::mutex> g(ws.mu);
+    // argument errors first (upstream precedence), without a device
+    std::vector<uint32_t> &hm = ws.masks;
+    hm.resize((size_t)nobj);
+    for (int o = 0; o < nobj; ++o) {
+        const uint32_t mask = (uint32_t)present_mask(present + (size_t)o * n, n);
+        const int32_t slot = ah->h_pat[mask];
+        if (slot == kPatTooFew) return RSGPU_ERR_TOO_FEW_SHARDS;
+        if (slot == kPatSingular) return RSGPU_ERR_SINGULAR;
+        hm[o] = mask;
+    }
+    if ((e = ctx->use_device())) return e;
+    AtlasView A;
+    if ((e = ctx->atlas_view(mode, A))) return e;
+    const unsigned si = ws.next++ % MultiWorkspace::kRing;
+    MultiWorkspace::Slot &w = ws.slot[si];
+    if (!ws.upload) HIP_TRY(hipStreamCreateWithFlags(&ws.upload, hipStreamNonBlocking));
+    if (!ws.uploaded[si]) HIP_TRY(hipEventCreateWithFlags(&ws.uploaded[si], hipEventDisableTiming));
+    if (w.done) HIP_TRY(hipEventSynchronize(w.done));  // the kernels that read it kRing calls ago
+    else HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+    const size_t bytes = (size_t)nobj * 4;
+    if (w.cap < bytes) {
+        if (w.d) (void)hipFree(w.d);
+        if (w.h) (void)hipHostFree(w.h);
+        w.d = nullptr;
+        w.h = nullptr;
+        w.cap = 0;
+        const size_t cap = std::max<size_t>(bytes * 2, 1 << 16);
+        HIP_TRY(hipMalloc(&w.d, cap));
+        HIP_TRY(hipHostMalloc(&w.h, cap, hipHostMallocDefault));
+        w.cap = cap;
+    }
+    std::memcpy(w.h, hm.data(), bytes);
+    HIP_TRY(hipMemcpyAsync(w.d, w.h, bytes, hipMemcpyHostToDevice, ws.upload));
+    HIP_TRY(hipEventRecord(ws.uploaded[si], ws.upload));
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, ws.uploaded[si], 0));
+    Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
+    e = run_masked(ctx, A, mode, L, (const uint32_t *)w.d, mode == kAtlasDecode ? d_bad : nullptr,
+                   (hipStream_t)stream);
+    // the slot is reused only after these kernels finished with the masks
+    const hipError_t he = hipEventRecord(w.done, (hipStream_t)stream);
+    if (e) return e;
+    if (he != hipSuccess) return hip_fail(he, "multi ring event");
+    return RSGPU_OK;
+}
+
 static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                            size_t pitch, size_t obj_stride, int nobj, bool data_only, bool check,
                            uint32_t *d_bad, void *stream) {
@@ -622,6 +857,11 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
     const int n = ctx->n;
+    if (nobj == 0) return RSGPU_OK;
+    if (n <= kAtlasMaxN)
+        return recon_dev_multi_atlas(ctx, d_base, present, shard_len, pitch, obj_stride, nobj,
+                                     check ? kAtlasDecode : data_only ? kAtlasData : kAtlasReconstruct, d_bad,
+                                     stream);
     // pattern key: the present bitmask (n <= 64: one word, looked up in a
     // PatternTable — a Get batch of 4 KiB objects holds 10^5+ objects, and
     // this loop is host time in front of the launch; else a byte string)
@@ -685,6 +925,18 @@ int rsgpu_decode_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     if (!d_bad) return RSGPU_ERR_INVALID_ARG;
     return recon_dev_multi(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, false, true, d_bad,
                            stream);
+}
+
+int rsgpu_decode_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len,
+                           size_t pitch, size_t obj_stride, int nobj, uint32_t *d_status, void *stream) {
+    return dev_masks(ctx, d_base, d_masks, shard_len, pitch, obj_stride, nobj, kAtlasDecode, d_status, stream);
+}
+
+int rsgpu_reconstruct_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len,
+                                size_t pitch, size_t obj_stride, int nobj, int data_only, uint32_t *d_status,
+                                void *stream) {
+    return dev_masks(ctx, d_base, d_masks, shard_len, pitch, obj_stride, nobj,
+                     data_only ? kAtlasData : kAtlasReconstruct, d_status, stream);
 }
 
 int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,

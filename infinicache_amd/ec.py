@@ -335,6 +335,20 @@ class RSEncoder:
         _check(self._L.rsgpu_decode_dev_multi(self._ctx, _dptr(base), pp, shard_len, pitch,
                                               obj_stride, nobj, _dptr(bad), _stream_handle(stream)))
 
+    def decode_dev_masks(self, base, masks, shard_len, pitch, obj_stride, nobj, status, stream=None):
+        """Per-object erasure patterns as device-resident present bitmasks
+        (masks: nobj uint32 in HBM, bit i = shard i arrived); the pattern ->
+        pass resolution runs on the device.  status (nobj uint32 in HBM):
+        0 ok, 1 Verify-after-Reconstruct mismatch, 2 too few shards, 3 singular."""
+        _check(self._L.rsgpu_decode_dev_masks(self._ctx, _dptr(base), _dptr(masks), shard_len, pitch,
+                                              obj_stride, nobj, _dptr(status), _stream_handle(stream)))
+
+    def reconstruct_dev_masks(self, base, masks, shard_len, pitch, obj_stride, nobj, data_only=False,
+                              status=None, stream=None):
+        _check(self._L.rsgpu_reconstruct_dev_masks(self._ctx, _dptr(base), _dptr(masks), shard_len, pitch,
+                                                   obj_stride, nobj, int(data_only), _dptr(status),
+                                                   _stream_handle(stream)))
+
     # -- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
     def encode_batch(self, objs: Sequence) -> None:
         """Encode many objects, each given as its Split() result (or the

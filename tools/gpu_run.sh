@@ -26,6 +26,13 @@ for s in $STEPS; do
             run bench_enc 300 python bench.py --workload enc --no-cpu
             run bench_dec4 300 python bench.py --workload dec4 --no-cpu
             run bench_mixed 300 python bench.py --workload encdec_mixed --no-cpu ;;
+    masks)  run pytest_masks 600 python -u -m pytest tests/test_gpu_masks.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    mixed)  for wl in small_mixed encdec_mixed small; do
+              run bench_$wl 300 python bench.py --workload $wl --no-cpu
+            done ;;
+    prof_mixed) for wl in small_mixed encdec_mixed; do
+              run prof_$wl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 --workload $wl
+            done ;;
     pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
     torchrun1) run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --no-cpu ;;
