@@ -34,51 +34,9 @@
 #include "gf_apply.h"
 #include "gf256.h"
 #include "gf_device.h"
-#include "gf_masked.h"
+#include "gf_launch.h"
 
 namespace rsgpu {
-
-// Tuned launch shape of the specialised pass (tools/kbench.hip sweeps on
-// MI355X), measured on COLD batches: every timed launch reads a
-// batch copy that no launch has touched within the last ~4 GB of traffic, so
-// nothing of it is still in the 256 MiB Infinity Cache (KB_ROT=4).  A batch
-// that is re-coded back to back instead (the same 1.3 GB every launch) gets
-// its parity rewrites absorbed by that cache; that warm rate is not the HBM
-// rate and is not what the policy is tuned for.
-//   * 256 lanes x one 16-B vector per row (128/512/1024 lanes, 2-4 vectors
-//     per lane and walking 2-8 chunks per workgroup are all <= this);
-//   * non-temporal (nt) input loads: every input byte is read exactly once;
-//   * nt stores: 70.1 vs 67.9 % (sc1) cold on RS(10+2) encode (sc1 wins only
-//     warm: 80 vs 70 %, the Infinity Cache absorbing repeated parity writes);
-//   * XCD-contiguous workgroup order for every launch: 72.7 vs 70.0 % (linear)
-//     cold; splitting each XCD's share into 2-32 interleaved regions loses
-//     1-9 points (gf_device.h Order).
-constexpr int kBlock = 256;    // lanes per workgroup
-constexpr int kUnroll = 1;     // 16-B vectors per lane
-constexpr int kLoadAux = 2;    // buffer_load: nt
-constexpr int kStoreAux = 2;   // buffer_store: nt
-constexpr int kMultiChunks = 1; // chunks per workgroup in the mixed-pattern kernel (kbench: 1 best)
-// launches whose objects span more than this use the XCD-contiguous workgroup
-// order (gf_device.h Order); 0: every launch
-constexpr size_t kXcdSpan = 0;
-// Occupancy cap for passes that store rows.  The kernels use no LDS, so a
-// dynamic LDS reservation of 1/W of the CU's 160 KiB caps residency at W
-// workgroups (4 waves each) per CU.  Fewer concurrent row streams keep DRAM
-// pages open longer; the best W keeps about 160 KiB of input loads in flight
-// per CU (K rows x 4 KiB per workgroup): W = 40 / K, clamped to [2, 8]
-// (tools/kbench KB_SET=occ, cold, r01_kbench_cold_occ_*):
-//   encode RS(8+4)   W=4: 75.9 vs 73.2 % full occupancy
-//   encode RS(10+2)  W=4: 74.0 vs 72.5 %; ReconstructData RS(10+4) 75.0 vs 73.9 %
-//   encode RS(12+4)  W=3: 73.4 vs 68.5 % (W=2: 74.1)
-//   encode RS(16+4)  W=2: 77.8 vs 73.7 %;  encode RS(16+2) W=2: 80.1 vs 76.4 %
-// Check-only passes (Verify) keep full occupancy: the VALU-bound RS(10+4)
-// verify drops from 84.3 to 77.7 % under a cap of 4.
-constexpr unsigned store_lds(int K) {
-    const int w = K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K);
-    return 160u * 1024u / (unsigned)w - 256u;
-}
-constexpr int kMaxK = 16;  // specialised kernels cover K <= 16
-constexpr int kMaxR = 4;   // and up to 4 output rows per pass
 
 static_assert(kTabWords == kCoefWords, "host and device table formats differ");
 
@@ -201,23 +159,6 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
 // ----------------------------------------------------------------- launchers
 
 namespace {
-
-// 1D launch over nitem items x nchunk workgroups; `span` = bytes the launch's
-// objects cover.  Returns the order and sets the grid size.
-Order make_order(uint32_t nchunk, uint32_t nitem, size_t span, unsigned &grid) {
-    Order o{nchunk, nchunk * nitem, 0};
-    if (span > kXcdSpan && o.total >= 8) o.xper = (o.total + 7) / 8;
-    grid = o.xper ? o.xper * 8 : o.total;
-    return o;
-}
-
-// items per launch so that the 1D grid stays below 2^31 workgroups
-int max_items(unsigned nchunk) { return (int)std::max(1u, 0x7ff00000u / std::max(1u, nchunk)); }
-
-// bytes covered by `no` objects of layout L (one object: its own span)
-size_t objs_span(const Layout &L, int no, size_t one) {
-    return no > 1 ? (size_t)no * L.obj_stride : one;
-}
 
 struct Sub {  // one pass over <= kMaxR output rows of a plan
     int r0, R, nw;
@@ -574,152 +515,6 @@ hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
-}
-
-// ------------------------------------------- device-resolved mixed patterns
-
-namespace {
-
-template <int KMAX, int R>
-hipError_t launch_masked_t(const AtlasView &A, const Layout &L, const uint32_t *masks, uint32_t *status,
-                           uint32_t *acc, uint32_t *cnt, hipStream_t st) {
-    MaskedArgs a{};
-    a.obj_stride = L.obj_stride;
-    a.pat = A.pat;
-    a.recs = (const PatRec *)A.recs;
-    a.tabs = A.tabs;
-    a.ctab = A.ctab;
-    a.nmask = (uint32_t)((1ull << A.n) - 1);
-    a.kfix = (uint32_t)A.kfix;
-    a.nsub = (uint32_t)A.nsub;
-    a.nvec = (uint32_t)((L.shard_len + 15) / 16);
-    a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
-    a.pitch = (uint32_t)L.pitch;
-    a.span = (uint32_t)((size_t)(A.n - 1) * L.pitch + (size_t)a.nvec * 16);
-    a.nobj = (uint32_t)L.nobj;
-    // occupancy cap for the common pattern (a healthy Get: k inputs, rows written)
-    const unsigned cap = store_lds(A.kcap);
-    // Short rows: a workgroup codes opw whole objects (gf_apply_lanes), all
-    // lanes addressing them from the group's first object in one 32-bit range
-    uint32_t opw = 1;
-    if (a.nvec * 2 <= kBlock) {
-        opw = kBlock / a.nvec;
-        while (opw > 1 && (uint64_t)(opw - 1) * L.obj_stride + a.span >= 0x7fffffffull) opw /= 2;
-    }
-    for (int s = 0; s < A.nsub; ++s) {
-        a.sub = (uint32_t)s;
-        if (opw > 1) {
-            a.opw = opw;
-            a.gspan = (uint32_t)((uint64_t)(opw - 1) * L.obj_stride + a.span);
-            constexpr unsigned stat = sizeof(u32x4) * 256 * 2 + 4 * 256;  // gf_apply_lanes' static LDS
-            const unsigned dyn = cap > stat ? cap - stat : 0u;
-            const size_t groups = ((size_t)L.nobj + opw - 1) / opw;
-            for (size_t g0 = 0; g0 < groups; g0 += (size_t)max_items(1)) {
-                const size_t ng = std::min((size_t)max_items(1), groups - g0);
-                const size_t o0 = g0 * opw;
-                a.base = L.base + o0 * L.obj_stride;
-                a.masks = masks + o0;
-                a.status = status ? status + o0 : nullptr;
-                a.acc = acc ? acc + o0 : nullptr;
-                a.cnt = cnt ? cnt + o0 : nullptr;
-                a.nobj = (uint32_t)std::min<size_t>(ng * opw, (size_t)L.nobj - o0);
-                unsigned grid;
-                a.ord = make_order(1, (uint32_t)ng, (size_t)a.nobj * L.obj_stride, grid);
-                hipLaunchKernelGGL((gf_apply_lanes<KMAX, R, kLoadAux, kStoreAux>), dim3(grid), dim3(kBlock), dyn, st, a);
-                hipError_t e = hipGetLastError();
-                if (e != hipSuccess) return e;
-            }
-            continue;
-        }
-        const unsigned gx = (a.nvec + kBlock - 1) / kBlock;
-        const int step = max_items(gx);
-        for (int o0 = 0; o0 < L.nobj; o0 += step) {
-            const int no = std::min(step, L.nobj - o0);
-            a.base = L.base + (size_t)o0 * L.obj_stride;
-            a.masks = masks + o0;
-            a.status = status ? status + o0 : nullptr;
-            a.acc = acc ? acc + o0 : nullptr;
-            a.cnt = cnt ? cnt + o0 : nullptr;
-            a.opw = 1;
-            a.gspan = 0;
-            unsigned grid;
-            a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
-            hipLaunchKernelGGL((gf_apply_masked<KMAX, R, kLoadAux, kStoreAux>), dim3(grid), dim3(kBlock), cap, st, a);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
-        }
-    }
-    return hipSuccess;
-}
-
-typedef hipError_t (*masked_fn)(const AtlasView &, const Layout &, const uint32_t *, uint32_t *, uint32_t *,
-                                uint32_t *, hipStream_t);
-
-template <int K>
-masked_fn pick_masked_r(int R) {
-    return R == 1 ? &launch_masked_t<K, 1> : R == 2 ? &launch_masked_t<K, 2>
-         : R == 3 ? &launch_masked_t<K, 3> : &launch_masked_t<K, 4>;
-}
-
-masked_fn pick_masked(int K, int R) {
-    switch (K) {
-#define RSGPU_K(k) case k: return pick_masked_r<k>(R);
-        RSGPU_K(1) RSGPU_K(2) RSGPU_K(3) RSGPU_K(4) RSGPU_K(5) RSGPU_K(6) RSGPU_K(7) RSGPU_K(8)
-        RSGPU_K(9) RSGPU_K(10) RSGPU_K(11) RSGPU_K(12) RSGPU_K(13) RSGPU_K(14) RSGPU_K(15)
-        RSGPU_K(16)
-#undef RSGPU_K
-        default: return nullptr;
-    }
-}
-
-}  // namespace
-
-hipError_t launch_masked(const AtlasView &A, const Layout &L, const uint32_t *d_masks, uint32_t *d_status,
-                         uint32_t *acc, uint32_t *cnt, hipStream_t st) {
-    if (L.nobj <= 0) return hipSuccess;
-    if (L.in_base || L.out_base || (L.pitch % 16) != 0 || A.R < 1 || A.R > kMaxR) return hipErrorInvalidValue;
-    masked_fn f = pick_masked(A.kmax, A.R);
-    if (!f) return hipErrorInvalidValue;
-    return f(A, L, d_masks, d_status, acc, cnt, st);
-}
-
-hipError_t StatusScratch::acquire(size_t nobj, hipStream_t stream, Slot *&s) {
-    mu.lock();  // held until release(): one call in flight per ring position
-    s = &slot[next++ % kRing];
-    hipError_t e = hipSuccess;
-    if (s->done) e = hipEventSynchronize(s->done);  // the call that used it kRing calls ago
-    else e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
-    if (e == hipSuccess && s->cap < nobj) {
-        if (s->d) (void)hipFree(s->d);
-        s->d = nullptr;
-        s->cap = 0;
-        const size_t cap = std::max<size_t>(nobj, 1024);
-        e = hipMalloc(&s->d, cap * 2 * sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMemsetAsync(s->d, 0, cap * 2 * sizeof(uint32_t), stream);
-        if (e == hipSuccess) s->cap = cap;
-    }
-    if (e != hipSuccess) mu.unlock();
-    return e;
-}
-
-hipError_t StatusScratch::release(Slot *s, hipStream_t stream, bool ok) {
-    hipError_t e = ok ? hipEventRecord(s->done, stream) : hipSuccess;
-    if (!ok || e != hipSuccess) {
-        // a failed launch may leave counters set: re-zero on the next use
-        (void)hipStreamSynchronize(stream);
-        if (s->d) (void)hipFree(s->d);
-        s->d = nullptr;
-        s->cap = 0;
-    }
-    mu.unlock();
-    return e;
-}
-
-StatusScratch::~StatusScratch() {
-    for (auto &s : slot) {
-        if (s.done) (void)hipEventDestroy(s.done);
-        if (s.d) (void)hipFree(s.d);
-    }
 }
 
 MultiWorkspace::~MultiWorkspace() {

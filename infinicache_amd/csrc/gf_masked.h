@@ -13,20 +13,23 @@
 //
 //   * gf_apply_masked (rows of > 128 vectors): one workgroup = 256 lanes x
 //     16 B of one object chunk, as gf_apply_kernel.  The object's mask, its
-//     atlas slot and the slot's coefficient tables come through scalar loads;
-//     the input rows (the first kact present rows in index order: upstream's
-//     survivor rule followed by the fused decode's extra shards) are the set
-//     bits of the mask, found with s_ff1 — no table needed for them.
+//     atlas slot and the slot's record (input rows: the first kact present
+//     rows in index order, upstream's survivor rule followed by the fused
+//     decode's extra shards; written rows; coefficient tables) come through
+//     scalar loads.
 //   * gf_apply_lanes (rows of <= 128 vectors, small objects): one workgroup
 //     codes opw = 256 / nvec whole objects in address order, lane -> (object,
 //     vector), exactly as the uniform small-object launch, whatever their
-//     patterns.  Each lane resolves its own object's pattern and indexes a
-//     256-entry coefficient table staged in LDS by the coefficient bytes of
-//     its pattern (v_perm takes its table words from VGPRs anyway).
+//     patterns.  Each lane resolves its own object's pattern (input rows =
+//     the set bits of its mask) and indexes a 256-entry coefficient table
+//     staged in LDS by the coefficient bytes of its pattern (v_perm takes its
+//     table words from VGPRs anyway).
 //
 // Inputs beyond an object's kact read through a zero-record buffer resource
 // (or past every range): the load returns zero and touches no memory.
 #pragma once
+#include <cstddef>
+
 #include "gf_device.h"
 
 namespace rsgpu {
@@ -45,8 +48,11 @@ struct alignas(16) PatRec {
     uint8_t out_row[4];  // written rows (shard indices)
     uint8_t pad1[4];
     uint8_t coef[4][16];  // [r][c], zero for r >= nr or c >= kact
+    uint8_t in_row[16];   // input rows: the first kact present rows, ascending (gf_apply_masked)
 };
-static_assert(sizeof(PatRec) == 80, "PatRec layout (host atlas builder and lanes kernel loads)");
+static_assert(sizeof(PatRec) == 96 && offsetof(PatRec, out_row) == 8 && offsetof(PatRec, coef) == 16 &&
+                  offsetof(PatRec, in_row) == 80,
+              "PatRec layout (host atlas builder, dword reads in both kernels)");
 
 // pattern-table entries besides a record slot
 constexpr int32_t kPatTooFew = -1;   // fewer than data shards present: ErrTooFewShards (status 2)
@@ -116,8 +122,14 @@ __global__ __launch_bounds__(256) void gf_apply_masked(const MaskedArgs a) {
         return;
     }
     const uint32_t ri = (uint32_t)slot * a.nsub + a.sub;
-    const __attribute__((address_space(4))) PatRec &rc = ((constant_ptr<PatRec>)a.recs)[ri];
-    const uint32_t kact = rc.kact, nr = rc.nr, nw = rc.nw, ki = rc.ki, nchk = rc.nchk;
+    // the record as dwords (scalar loads are dword-granular; byte fields
+    // would go through vector loads): [0] kact|nr|nw|ki, [1] nchk,
+    // [2] out_row[0..3], [20..23] in_row[0..15]
+    const constant_ptr<uint32_t> rw = (constant_ptr<uint32_t>)((constant_ptr<PatRec>)a.recs + ri);
+    const uint32_t h0 = rw[0], h1 = rw[1], orow = rw[2];
+    const uint32_t irow[4] = {rw[20], rw[21], rw[22], rw[23]};
+    const uint32_t kact = h0 & 0xffu, nr = (h0 >> 8) & 0xffu, nw = (h0 >> 16) & 0xffu, ki = h0 >> 24;
+    const uint32_t nchk = h1 & 0xffu;
     if (nchk == 0 && a.sub == 0 && chunk == 0 && t == 0 && a.status) a.status[obj] = kStatusOk;
     if (nr == 0) return;
     const constant_ptr<uint32_t> tb = (constant_ptr<uint32_t>)a.tabs + (size_t)ri * (KMAX * R * kTabWords);
@@ -130,15 +142,16 @@ __global__ __launch_bounds__(256) void gf_apply_masked(const MaskedArgs a) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, 0, 0x00020000);
 
-    // input rows = the first kact set bits of the mask, ascending
+    // input rows (the record's, scalar): every load is issued, unused inputs
+    // through the zero-record resource, so the wait counts stay static
     u32x4 x[KMAX];
-    uint32_t m = mask;
 #pragma unroll
-    for (int c = 0; c < KMAX; ++c) {
-        const uint32_t row = m ? (uint32_t)__builtin_ctz(m) : 0u;
-        m &= m - 1u;
-        x[c] = __builtin_amdgcn_raw_buffer_load_b128((uint32_t)c < kact ? rs : rsn, voff, row * a.pitch, LAUX);
-    }
+    for (int c = 0; c < KMAX; ++c)
+        x[c] = __builtin_amdgcn_raw_buffer_load_b128((uint32_t)c < kact ? rs : rsn, voff,
+                                                     ((irow[c >> 2] >> (8 * (c & 3))) & 0xffu) * a.pitch, LAUX);
+    // keep every load here, in input order: otherwise each one is sunk into
+    // the `c < kact` block that uses it, and input 0 is fetched last
+    asm volatile("" ::: "memory");
 
     uint32_t acc[R][4];
 #pragma unroll
@@ -149,12 +162,13 @@ __global__ __launch_bounds__(256) void gf_apply_masked(const MaskedArgs a) {
     for (int c = 0; c < KMAX; ++c) {
         if ((uint32_t)c < kact) {
             if ((uint32_t)c + ki < kact) {
+                // every row: rows past nr have zero tables (no per-row branches,
+                // which would re-fetch the tables inside the dword loop)
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
                     const GfIdx g = gf_idx(x[c][d]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        if ((uint32_t)r < nr) acc[r][d] = gf_mac(acc[r][d], tb + (c * R + r) * kTabWords, g);
+                    for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], tb + (c * R + r) * kTabWords, g);
                 }
             } else {
                 // identity input (Verify's parity columns, the decode's extras):
@@ -181,7 +195,7 @@ __global__ __launch_bounds__(256) void gf_apply_masked(const MaskedArgs a) {
         if ((uint32_t)r < nw) {
             if (lane_ok) {
                 u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, (uint32_t)rc.out_row[r] * a.pitch, SAUX);
+                __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, ((orow >> (8 * r)) & 0xffu) * a.pitch, SAUX);
             }
         } else if (lane_ok) {
             const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
@@ -227,6 +241,7 @@ __global__ __launch_bounds__(256) void gf_apply_lanes(const MaskedArgs a) {
         x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)c < kact ? lane_off + row * a.pitch : 0xfffffff0u,
                                                      0u, LAUX);
     }
+    asm volatile("" ::: "memory");  // loads stay here, in input order (see gf_apply_masked)
     // the lane's record: header (kact, nr, nw, ki | nchk | out_row) and coefficient rows
     const u32x4 *rp = (const u32x4 *)(a.recs + (size_t)(act ? (uint32_t)slot : 0u) * a.nsub + a.sub);
     const u32x4 zero = {0u, 0u, 0u, 0u};
@@ -254,7 +269,6 @@ __global__ __launch_bounds__(256) void gf_apply_lanes(const MaskedArgs a) {
             for (int d = 0; d < 4; ++d) g[d] = gf_idx(x[c][d]);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                if (__builtin_amdgcn_ballot_w64((uint32_t)r < nr) == 0) continue;
                 // coefficient (r, c) of this lane's pattern (zero where unused)
                 const uint32_t cf = (crow[r][c >> 2] >> (8 * (c & 3))) & 0xffu;
                 const u32x4 tw = lt[cf][0];

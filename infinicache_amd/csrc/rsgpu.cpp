@@ -289,7 +289,7 @@ int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
     struct Ent {
         int K, R, nw, ki;
         std::vector<uint8_t> coef;
-        std::vector<int> out_rows;
+        std::vector<int> out_rows, in_rows;
     };
     std::vector<int32_t> pat(nm);
     std::vector<Ent> ents;
@@ -322,7 +322,7 @@ int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
             continue;
         }
         pat[mask] = (int32_t)ents.size();
-        ents.push_back({pl.K, pl.R, pl.nw, pl.identity_inputs(), pl.coef, pl.out_rows});
+        ents.push_back({pl.K, pl.R, pl.nw, pl.identity_inputs(), pl.coef, pl.out_rows, pl.in_rows});
         maxR = std::max(maxR, pl.R);
     }
     const int R = std::max(1, std::min(4, maxR)), nsub = std::max(1, (maxR + 3) / 4);
@@ -351,6 +351,7 @@ int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
             // identity inputs feed the plan's last rows: usable in its last sub-pass
             rc.ki = (uint8_t)(nr > 0 && r0 + nr == e.R ? std::min(e.ki, nr) : 0);
             rc.nchk = (uint8_t)nchk;
+            for (int c = 0; c < e.K; ++c) rc.in_row[c] = (uint8_t)e.in_rows[c];
             uint32_t *tb = &tabs[(i * nsub + s) * tw];
             for (int r = 0; r < nr; ++r) {
                 if (r < nw) rc.out_row[r] = (uint8_t)e.out_rows[r0 + r];

@@ -7,7 +7,6 @@ import os
 import re
 import subprocess
 import sys
-import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,18 +14,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     lib = os.path.join(ROOT, "infinicache_amd", "librsgpu.so")
-    with tempfile.TemporaryDirectory() as d:
-        subprocess.run([f"{LLVM}/llvm-objdump", "--offloading", lib], cwd=d, check=True,
-                       stdout=subprocess.DEVNULL)
-        cos = [f for f in os.listdir(os.path.dirname(lib)) if f.startswith("librsgpu.so.0.hipv4")]
-        co = os.path.join(os.path.dirname(lib), cos[0])
-        try:
-            notes = subprocess.run([f"{LLVM}/llvm-readobj", "--notes", co], capture_output=True,
-                                   text=True, check=True).stdout
-        finally:
-            for f in os.listdir(os.path.dirname(lib)):
-                if f.startswith("librsgpu.so.0."):
-                    os.remove(os.path.join(os.path.dirname(lib), f))
+    libdir = os.path.dirname(lib)
+    notes = ""
+    subprocess.run([f"{LLVM}/llvm-objdump", "--offloading", lib], check=True, stdout=subprocess.DEVNULL)
+    try:  # one code object per HIP translation unit, extracted next to the library
+        for f in sorted(os.listdir(libdir)):
+            if f.startswith("librsgpu.so.") and "amdgcn" in f:
+                notes += subprocess.run([f"{LLVM}/llvm-readobj", "--notes", os.path.join(libdir, f)],
+                                        capture_output=True, text=True, check=True).stdout
+    finally:
+        for f in os.listdir(libdir):
+            if f.startswith("librsgpu.so.") and f != "librsgpu.so":
+                os.remove(os.path.join(libdir, f))
     pats = sys.argv[1:]
     for e in notes.split("- .agpr_count")[1:]:
         name = re.search(r"\.name:\s+(\S+)", e).group(1)
