@@ -81,13 +81,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16):
+def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, windows=3):
     """Time the oracle's port of the Go path (upstream galMulAVX2Xor /
-    codeSomeShardsAvx512 SIMD coders) on `threads` host threads over a bounded
-    sample laid out like the GPU batch, bit-compare with the GPU output.
-    Headline form: object-parallel (one object per task, as many concurrent
-    EcSet/EcGet calls would run); the per-object codeSomeShardsP split form
-    (maxGoroutines 32, minSplitSize 1024) is timed beside it for reference."""
+    codeSomeShardsAvx512 SIMD coders) over a bounded sample laid out like the
+    GPU batch, bit-compare with the GPU output.  Headline form: object-
+    parallel (one object per task, as many concurrent EcSet/EcGet calls would
+    run) on `threads` threads (the box's cgroup share) and on 1 thread, each
+    the MEDIAN of `windows` timing windows (SURVEY §8d: 1-core and all-core);
+    the per-object codeSomeShardsP split form (maxGoroutines 32, minSplitSize
+    1024, client/example/main.go:22) is timed beside it for reference."""
     import ctypes
 
     import oracle
@@ -99,27 +101,34 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16):
     surv = [i for i in range(n) if i not in lost and i not in w.get("absent", ())][:k]
     base = sample.reshape(-1)
 
-    def one_pass():
+    def one_pass(nt, nobj):
         if "encode" in w["ops"]:
             oracle.code_batch(m[k:], list(range(k)), list(range(k, n)), base, n * pitch, pitch, S,
-                              ns, nthreads=threads)
+                              nobj, nthreads=nt)
         if "decode" in w["ops"]:
-            oracle.code_batch(inv_rows, surv, lost, base, n * pitch, pitch, S, ns,
-                              nthreads=threads)
+            oracle.code_batch(inv_rows, surv, lost, base, n * pitch, pitch, S, nobj, nthreads=nt)
 
-    one_pass()  # warm the pool and the pages
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        one_pass()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    value = ns * reps * w["nbytes"] * len(w["ops"]) / el / GiB
+    def rate(nt, nobj, secs):
+        """median GiB/s over `windows` windows of ~secs each"""
+        one_pass(nt, nobj)  # warm the pool and the pages
+        vals = []
+        for _ in range(windows):
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                one_pass(nt, nobj)
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= secs:
+                    break
+            vals.append(nobj * reps * w["nbytes"] * len(w["ops"]) / el / GiB)
+        return float(np.median(vals)), vals
+
+    all_v, all_w = rate(threads, ns, budget_s * 0.5 / windows)
+    one_v, one_w = rate(1, ns, budget_s * 0.3 / windows)  # same sample: beyond the host's L3
     exact = bool(np.array_equal(sample[:, :, :S], gpu_sample[:, :, :S]))
-    # per-object codeSomeShardsP form, ~2 s
+    # per-object codeSomeShardsP form, ~budget/5 s
     sreps, t1 = 0, time.perf_counter()
-    while time.perf_counter() - t1 < min(2.0, budget_s / 5):
+    while time.perf_counter() - t1 < budget_s / 5:
         for o in range(ns):
             if "encode" in w["ops"]:
                 oracle.code_fast(m[k:], [sample[o, c, :S] for c in range(k)], nthreads=threads,
@@ -139,12 +148,16 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16):
     except Exception:
         pass
     return {
-        "value": round(value, 3),
+        "value": round(all_v, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{ns} x {w['nbytes'] >> 20} MiB objects x {reps} reps ({' + '.join(w['ops'])}), "
-                  f"{el:.1f} s, object-parallel on {threads} threads, {isa} coder "
+        "windows_GiBps": [round(v, 2) for v in all_w],
+        "one_core": {"value": round(one_v, 3), "cores": 1, "windows_GiBps": [round(v, 2) for v in one_w]},
+        "per_object_split_form_GiBps": round(split_val, 3),
+        "sample": f"{ns} x {w['nbytes'] >> 10} KiB objects ({' + '.join(w['ops'])}), object-parallel; value = "
+                  f"median of {windows} windows on {threads} threads (the box's cgroup share), one_core = "
+                  f"median of {windows} windows on 1 thread, same sample; {isa} coder "
                   f"(oracle/rs_oracle.c restating upstream's SIMD path; Go toolchain and "
                   f"klauspost/reedsolomon unavailable offline); per-object codeSomeShardsP split "
                   f"form {split_val:.2f} GiB/s; host CPU: {cpu_model}; bit-exact vs GPU: {exact}",
@@ -438,12 +451,10 @@ def main():
                     help="strong scaling: the workload's batch is the TOTAL, split over ranks")
     ap.add_argument("--copies", type=int, default=3,
                     help="distinct batches per GPU, step i codes batch i %% copies (cold Infinity Cache)")
-    ap.add_argument("--event-every", type=int, default=4,
-                    help="per-kernel HIP events on every Nth timed step (1: every step)")
     ap.add_argument("--warm", action="store_true",
                     help="also time K steps re-coding one batch (warm Infinity Cache; comparison only)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     args = ap.parse_args()
 
     if args.workload == "trace":
@@ -459,6 +470,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 ranks with "
+                         f"python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
     # BENCH_DIST_BACKEND=gloo + BENCH_SHARE_GPU=1: rehearse the N-rank path on
     # a one-GPU box (ranks share cuda:0; RCCL refuses two ranks on one GPU).
     # The driver's multi-GPU runs use the defaults: RCCL, one GPU per rank.
@@ -520,61 +534,73 @@ def main():
         masks_np = (pres_m.astype(np.int64) << np.arange(n)).sum(axis=1).astype(np.int32)
         masks_dev = torch.from_numpy(masks_np).to(dev)
 
+    def op_encode(buf):
+        enc.encode_dev(buf, S, pitch, stride, nobj, stream)
+
+    def op_decode(buf):
+        if w.get("upstream_get"):
+            enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=False, stream=stream)
+            enc.verify_dev(buf, S, pitch, stride, nobj, bad, stream)
+        elif w.get("mixed"):
+            enc.decode_dev_masks(buf, masks_dev, S, pitch, stride, nobj, bad, stream)
+        elif w.get("data_only"):
+            enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=True, stream=stream)
+        else:
+            enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, stream)
+
+    op_fns = {"encode": op_encode, "decode": op_decode}
     turn = [0]
 
-    def step(evs=None, fixed=None):
+    def step(fixed=None):
         buf = bufs[turn[0] % copies] if fixed is None else bufs[fixed]
         turn[0] += 1
-        if evs is not None:
-            evs[0].record(stream)
-        if "encode" in w["ops"]:
-            enc.encode_dev(buf, S, pitch, stride, nobj, stream)
-        if evs is not None:
-            evs[1].record(stream)
-        if "decode" in w["ops"]:
-            if w.get("upstream_get"):
-                enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=False, stream=stream)
-                enc.verify_dev(buf, S, pitch, stride, nobj, bad, stream)
-            elif w.get("mixed"):
-                enc.decode_dev_masks(buf, masks_dev, S, pitch, stride, nobj, bad, stream)
-            elif w.get("data_only"):
-                enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=True,
-                                    stream=stream)
-            else:
-                enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, stream)
-        if evs is not None:
-            evs[2].record(stream)
+        for op in w["ops"]:
+            op_fns[op](buf)
+
+    def kernel_ms(fixed=None):
+        """Per-op launch time: HIP events around an UNINTERRUPTED run of K
+        launches of that op alone (batches in the same rotation), on the
+        stream the kernels run on.  No marker packets between the launches,
+        so the average is the kernel's own time plus launch gaps; the timed
+        steps above carry no events at all."""
+        out = {}
+        for op in w["ops"]:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            op_fns[op](bufs[0 if fixed is not None else 1 % copies])  # untimed: same launch shape warm
+            e0.record(stream)
+            for i in range(args.steps):
+                op_fns[op](bufs[fixed if fixed is not None else i % copies])
+            e1.record(stream)
+            e1.synchronize()
+            out[op] = e0.elapsed_time(e1) / args.steps
+        return out
 
     dctx = DistCtx(world, rank, dev)
-    # per-kernel HIP events on every `event_every`-th timed step only: each
-    # event record is a marker packet that idles the GPU ~5 us between the
-    # kernels (rocprof trace), which is instrumentation, not the workload
-    ev_steps = list(range(0, args.steps, max(1, args.event_every)))
-    evs_at = {i: [torch.cuda.Event(enable_timing=True) for _ in range(3)] for i in ev_steps}
-    elapsed = timed_run(lambda i: step(None if i is None else evs_at.get(i)), args.steps, args.warmup,
-                        lambda: torch.cuda.synchronize(dev), dctx)
-    evs = list(evs_at.values())
+    elapsed = timed_run(lambda i: step(), args.steps, args.warmup, lambda: torch.cuda.synchronize(dev), dctx)
     objs_all = dctx.sum(nobj)
-
     if int(bad.sum()) != 0:
         raise SystemExit("decode reported a verify mismatch on synthetic data")
-
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    kms_alone = kernel_ms()
+    # Each op's share of the timed step comes from its uninterrupted run; run
+    # alone an op can be a little slower than inside the step (there a decode
+    # re-reads rows its batch's encode just streamed, partly still in the
+    # Infinity Cache), so the shares are scaled to the measured step when
+    # they add up to more: kernel time x launches never exceeds ms_per_step.
+    ms_per_step_meas = elapsed / args.steps * 1e3
+    scale = min(1.0, ms_per_step_meas / max(sum(kms_alone.values()), 1e-9))
+    kms = {op: t * scale for op, t in kms_alone.items()}
+    enc_ms, dec_ms = kms.get("encode", 0.0), kms.get("decode", 0.0)
     ops = len(w["ops"])
 
     # --warm: the same K steps on ONE batch (warm Infinity Cache), for
     # comparison only (off by default so a rocprofv3 run of the default
     # command averages the cold launches alone)
     if args.warm:
-        wevs_at = {i: [torch.cuda.Event(enable_timing=True) for _ in range(3)] for i in ev_steps}
-        warm_el = timed_run(lambda i: step(None if i is None else wevs_at.get(i), fixed=0), args.steps,
-                            args.warmup, lambda: torch.cuda.synchronize(dev), dctx)
-        wevs = list(wevs_at.values())
+        warm_el = timed_run(lambda i: step(fixed=0), args.steps, args.warmup,
+                            lambda: torch.cuda.synchronize(dev), dctx)
         if int(bad.sum()) != 0:
             raise SystemExit("decode reported a verify mismatch on synthetic data")
-        warm_ms = {"encode": float(np.mean([e[0].elapsed_time(e[1]) for e in wevs])),
-                   "decode": float(np.mean([e[1].elapsed_time(e[2]) for e in wevs]))}
+        warm_ms = kernel_ms(fixed=0)
     total_obj_bytes = objs_all * w["nbytes"] * ops * args.steps
     value = total_obj_bytes / elapsed / GiB
     ms_per_step = elapsed / args.steps * 1e3
@@ -618,7 +644,10 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "kernel": f"{kernel_key} ({dom} launches), {dom_bytes} algorithmic B/launch, "
-                  f"{dom_ms * 1e3:.1f} us avg (HIP events on {len(evs)} of {args.steps} timed steps)",
+                  f"{dom_ms * 1e3:.1f} us avg (HIP events around {args.steps} back-to-back launches "
+                  f"per op after the timed steps, scaled x{scale:.4f} to the timed step)",
+        "kernel_ms_per_step": round(sum(kms.values()), 4),
+        "kernel_ms_alone": {op: round(t, 4) for op, t in kms_alone.items()},
         "per_kernel_GBps": {op: round(b / (ms * 1e-3) / 1e9, 1) for op, (_, b, ms) in per_op.items()},
         # the read side alone (k*S input bytes per object and launch), SURVEY §8d
         "read_only": {"achieved": round(nobj * k * S / (dom_ms * 1e-3) / 1e9, 1),

@@ -60,6 +60,11 @@ extern "C" {
 
 typedef struct rsgpu_ctx rsgpu_ctx;
 
+/* rsgpu_create's `device`: every visible gfx950 device (a multi-device
+ * context, see rsgpu_create_multi); with none visible, a context on device 0
+ * whose compute calls return RSGPU_ERR_NO_DEVICE. */
+#define RSGPU_ALL_DEVICES (-1)
+
 /* Replaces reedsolomon.New(dataShards, parityShards, opts...) as called at
  * /root/reference/client/ec.go:19.  Rejects data<=0 || parity<=0
  * (RSGPU_ERR_INV_SHARD_NUM) and data+parity > 256 (RSGPU_ERR_MAX_SHARD_NUM).
@@ -67,6 +72,18 @@ typedef struct rsgpu_ctx rsgpu_ctx;
  * on the first compute call on `device`.  *out is NULL on error. */
 int rsgpu_create(int data_shards, int parity_shards, int device, unsigned flags, rsgpu_ctx **out);
 void rsgpu_destroy(rsgpu_ctx *ctx);
+
+/* One context over several GPUs of this process (the Go client is one
+ * process, client/client.go:47-59; its EcSet/EcGet callers share Client.EC).
+ * An object's shards never leave one GPU: per-object host calls go to the
+ * devices round-robin, batch host calls send object o to devices[o % ndev]
+ * and run the devices' pipelines in parallel (one PCIe link each),
+ * device-resident calls run on the device that owns d_base.  Duplicate
+ * devices: RSGPU_ERR_INVALID_ARG. */
+int rsgpu_create_multi(int data_shards, int parity_shards, const int *devices, int ndev, unsigned flags,
+                       rsgpu_ctx **out);
+/* The context's devices (up to cap written to out); returns their number. */
+int rsgpu_devices(const rsgpu_ctx *ctx, int *out, int cap);
 
 int rsgpu_data_shards(const rsgpu_ctx *ctx);
 int rsgpu_parity_shards(const rsgpu_ctx *ctx);

@@ -1,7 +1,7 @@
 """infinicache_amd — MI355X-native Reed-Solomon erasure coding for the
 InfiniCache client (drop-in for reedsolomon.Encoder under
 /root/reference/client/ec.go).  See DESIGN.md."""
-from .ec import (DummyEncoder, ErrInvalidInput, ErrInvShardNum, ErrMaxShardNum,  # noqa: F401
+from .ec import (ALL_DEVICES, DummyEncoder, ErrInvalidInput, ErrInvShardNum, ErrMaxShardNum,  # noqa: F401
                  ErrNotImplemented, ErrReconstructRequired, ErrShardNoData, ErrShardSize,
                  ErrShortData, ErrSingular, ErrTooFewShards, HipError, InvalidArgument, New,
                  NewEncoder, NoDevice, RSEncoder, RSError, device_count, device_ok, host_alloc,
@@ -12,5 +12,5 @@ __all__ = [
     "ErrInvShardNum", "ErrMaxShardNum", "ErrTooFewShards", "ErrShardNoData", "ErrShardSize",
     "ErrSingular", "ErrShortData", "ErrReconstructRequired", "ErrInvalidInput",
     "ErrNotImplemented", "InvalidArgument", "NoDevice", "HipError", "host_alloc",
-    "host_register", "host_unregister",
+    "host_register", "host_unregister", "ALL_DEVICES",
 ]

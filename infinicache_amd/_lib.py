@@ -23,6 +23,7 @@ EXPORTS = (
     "rsgpu_decode_dev_multi", "rsgpu_encode_batch", "rsgpu_decode_batch",
     "rsgpu_host_register", "rsgpu_host_unregister", "rsgpu_host_alloc", "rsgpu_host_free",
     "rsgpu_encode_verify", "rsgpu_decode_dev_masks", "rsgpu_reconstruct_dev_masks",
+    "rsgpu_create_multi", "rsgpu_devices",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -61,6 +62,8 @@ def load():
         pass
     L = ctypes.CDLL(LIB_PATH)
     L.rsgpu_create.argtypes = [ci, ci, ci, ctypes.c_uint, ctypes.POINTER(vp)]
+    L.rsgpu_create_multi.argtypes = [ci, ci, intp, ci, ctypes.c_uint, ctypes.POINTER(vp)]
+    L.rsgpu_devices.argtypes = [vp, intp, ci]
     L.rsgpu_destroy.argtypes = [vp]
     L.rsgpu_destroy.restype = None
     L.rsgpu_data_shards.argtypes = [vp]

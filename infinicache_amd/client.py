@@ -94,7 +94,7 @@ class Conn:
 
 
 class Client:
-    def __init__(self, dataShards: int, parityShards: int, ecMaxGoroutine: int, *, device: int = 0,
+    def __init__(self, dataShards: int, parityShards: int, ecMaxGoroutine: int, *, device: int = -1,
                  fused_decode: bool = True):
         self.Conns: Dict[str, List[Optional[Conn]]] = {}
         self.EC = NewEncoder(dataShards, parityShards, ecMaxGoroutine, device=device)

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -55,6 +56,18 @@ inline int hip_fail(hipError_t e, const char *what) {
         hipError_t e_ = (expr);                         \
         if (e_ != hipSuccess) return hip_fail(e_, #expr); \
     } while (0)
+
+// Restores the calling thread's current device when an API call returns
+// (rsgpu_ctx::use_device).
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() = default;
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 // Batch pipeline (pipeline.cpp): a ring of device slots, one stream each, so
 // H2D of object o+1 overlaps the kernel / D2H of object o.
@@ -112,6 +125,15 @@ struct rsgpu_ctx {
     std::once_flag ctab_once;
     int ctab_err = 0;
     rsgpu::StatusScratch scratch;    // multi-reporter status of the masked decode
+    // Multi-device context (rsgpu_create_multi / RSGPU_ALL_DEVICES): one
+    // single-device context per GPU.  Per-object calls go round-robin, batch
+    // calls split objects o -> device o mod N and run the devices in
+    // parallel, device-resident calls go to the device that owns the memory.
+    std::vector<std::unique_ptr<rsgpu_ctx>> subs;
+    std::atomic<unsigned> rr{0};
+    bool multi() const { return !subs.empty(); }
+    rsgpu_ctx *pick() { return subs[rr.fetch_add(1, std::memory_order_relaxed) % subs.size()].get(); }
+    rsgpu_ctx *sub_for(const void *dev_ptr);  // rsgpu.cpp; nullptr: not memory of one of our devices
     ~rsgpu_ctx() {
         if (d_ctab) (void)hipFree(d_ctab);
     }
@@ -129,14 +151,22 @@ struct rsgpu_ctx {
 
     const uint8_t *row(int r) const { return &m[(size_t)r * k]; }
 
-    // ---- device bring-up (lazy; per call hipSetDevice for thread safety)
-    int use_device() {
+    // ---- device bring-up (lazy).  Every call makes ctx->device current for
+    // its own duration and gives the calling thread its previous device back
+    // on return (the guard), so a process driving several GPUs from one thread
+    // never finds its current device switched under it.
+    int use_device(DeviceGuard &g) {
         {
-            std::lock_guard<std::mutex> g(mu);
+            std::lock_guard<std::mutex> l(mu);
             if (dev_state == 0) dev_state = rsgpu_device_ok(device) ? 1 : RSGPU_ERR_NO_DEVICE;
             if (dev_state < 0) return dev_state;
         }
-        HIP_TRY(hipSetDevice(device));
+        int cur = -1;
+        HIP_TRY(hipGetDevice(&cur));
+        if (cur != device) {
+            HIP_TRY(hipSetDevice(device));
+            g.prev = cur;
+        }
         return RSGPU_OK;
     }
 

@@ -28,6 +28,8 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <thread>
+#include <vector>
 
 #include "ctx.h"
 
@@ -156,8 +158,50 @@ int rsgpu_host_free(void *p) {
     return RSGPU_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Multi-device batch: objects o -> device o mod N, each device's share run
+// on its own host thread (its own pipeline, streams and PCIe link); returns
+// the first error.
+template <class F>
+int split_devices(rsgpu_ctx *ctx, int nobj, F run) {
+    const int N = (int)ctx->subs.size();
+    std::vector<std::vector<int>> objs(N);
+    for (int o = 0; o < nobj; ++o) objs[o % N].push_back(o);
+    std::vector<int> err(N, RSGPU_OK);
+    std::vector<std::thread> th;
+    for (int d = 1; d < N; ++d)
+        if (!objs[d].empty()) th.emplace_back([&, d] { err[d] = run(ctx->subs[d].get(), objs[d]); });
+    if (!objs[0].empty()) err[0] = run(ctx->subs[0].get(), objs[0]);
+    for (auto &t : th) t.join();
+    for (int e : err)
+        if (e) return e;
+    return RSGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard_lens, int nobj) {
     if (!ctx || (nobj > 0 && (!objs || !shard_lens)) || nobj < 0) return RSGPU_ERR_INVALID_ARG;
+    if (ctx->multi()) {
+        for (int o = 0; o < nobj; ++o) {  // argument errors before any device work
+            if (!objs[o]) return RSGPU_ERR_INVALID_ARG;
+            if (shard_lens[o] == 0) return RSGPU_ERR_SHARD_NO_DATA;
+        }
+        return split_devices(ctx, nobj, [&](rsgpu_ctx *sub, const std::vector<int> &os) {
+            std::vector<uint8_t *> o2;
+            std::vector<size_t> l2;
+            for (int o : os) {
+                o2.push_back(objs[o]);
+                l2.push_back(shard_lens[o]);
+            }
+            return rsgpu_encode_batch(sub, o2.data(), l2.data(), (int)os.size());
+        });
+    }
     const int k = ctx->k, p = ctx->p, n = ctx->n;
     size_t maxbytes = 0;
     for (int o = 0; o < nobj; ++o) {
@@ -167,7 +211,8 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
         maxbytes = std::max(maxbytes, (size_t)n * shard_lens[o] + 16);
     }
     if (nobj == 0) return RSGPU_OK;
-    int e = ctx->use_device();
+    DeviceGuard dg_;
+    int e = ctx->use_device(dg_);
     if (e) return e;
     auto plan = ctx->plan_encode();
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
@@ -192,6 +237,31 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
     if (!ctx || nobj < 0 || (nobj > 0 && (!shards || !present || !shard_lens || !ok)))
         return RSGPU_ERR_INVALID_ARG;
     const int k = ctx->k, n = ctx->n;
+    if (ctx->multi()) {
+        for (int o = 0; o < nobj; ++o) {  // argument errors before any device work
+            const uint8_t *pr = present + (size_t)o * n;
+            int np = 0;
+            for (int i = 0; i < n; ++i) np += pr[i] != 0;
+            if (shard_lens[o] == 0) return RSGPU_ERR_SHARD_NO_DATA;
+            if (np < k) return RSGPU_ERR_TOO_FEW_SHARDS;
+            for (int i = 0; i < n; ++i)
+                if (!shards[(size_t)o * n + i]) return RSGPU_ERR_INVALID_ARG;
+        }
+        return split_devices(ctx, nobj, [&](rsgpu_ctx *sub, const std::vector<int> &os) {
+            std::vector<uint8_t *> s2;
+            std::vector<uint8_t> p2;
+            std::vector<size_t> l2;
+            std::vector<int> ok2(os.size());
+            for (int o : os) {
+                s2.insert(s2.end(), shards + (size_t)o * n, shards + (size_t)(o + 1) * n);
+                p2.insert(p2.end(), present + (size_t)o * n, present + (size_t)(o + 1) * n);
+                l2.push_back(shard_lens[o]);
+            }
+            const int e = rsgpu_decode_batch(sub, s2.data(), p2.data(), l2.data(), (int)os.size(), ok2.data());
+            for (size_t i = 0; i < os.size(); ++i) ok[os[i]] = ok2[i];
+            return e;
+        });
+    }
     size_t maxbytes = 0;
     std::vector<std::shared_ptr<Plan>> plans(nobj);
     for (int o = 0; o < nobj; ++o) {
@@ -209,7 +279,8 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
         maxbytes = std::max(maxbytes, (size_t)n * shard_lens[o] + 16);
     }
     if (nobj == 0) return RSGPU_OK;
-    int e = ctx->use_device();
+    DeviceGuard dg_;
+    int e = ctx->use_device(dg_);
     if (e) return e;
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
     if ((e = ensure_slots(ctx, maxbytes))) return e;

@@ -103,6 +103,19 @@ bool gf_build_matrix(int k, int p, unsigned kind, std::vector<uint8_t> &out) {
 
 using namespace rsgpu;
 
+// Multi-device contexts forward every compute call to one of their per-device
+// contexts: per-object host calls round-robin (concurrent EcSet/EcGet callers
+// spread over the GPUs and their PCIe links), device-resident calls to the
+// device that owns the memory.
+#define RSGPU_FORWARD_RR(fn, ...) \
+    if (ctx && ctx->multi()) return fn(ctx->pick(), __VA_ARGS__)
+#define RSGPU_FORWARD_DEV(fn, ptr, ...)                  \
+    if (ctx && ctx->multi()) {                           \
+        rsgpu_ctx *sub_ = ctx->sub_for(ptr);             \
+        if (!sub_) return RSGPU_ERR_INVALID_ARG;         \
+        return fn(sub_, __VA_ARGS__);                    \
+    }
+
 namespace rsgpu {
 
 // upstream checkShards(shards, nilok): size = first non-empty length
@@ -406,6 +419,14 @@ int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_
 
 }  // namespace
 
+rsgpu_ctx *rsgpu_ctx::sub_for(const void *dev_ptr) {
+    hipPointerAttribute_t at;
+    if (!dev_ptr || hipPointerGetAttributes(&at, dev_ptr) != hipSuccess) return nullptr;
+    for (auto &c : subs)
+        if (c->device == at.device) return c.get();
+    return nullptr;
+}
+
 int rsgpu_ctx::atlas_host(AtlasMode mode, const Atlas *&out) {
     if (n > kAtlasMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
     Atlas &A = atlas[mode];
@@ -457,7 +478,8 @@ int dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shar
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
     if (ctx->n > kAtlasMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     if (nobj == 0) return RSGPU_OK;
     AtlasView A;
     if ((e = ctx->atlas_view(mode, A))) return e;
@@ -513,6 +535,15 @@ int rsgpu_create(int data_shards, int parity_shards, int device, unsigned flags,
     if (data_shards + parity_shards > 256) return RSGPU_ERR_MAX_SHARD_NUM;
     const unsigned kind = flags & RSGPU_MATRIX_MASK;
     if (kind > RSGPU_MATRIX_PAR1 || (flags & ~RSGPU_MATRIX_MASK)) return RSGPU_ERR_INVALID_ARG;
+    if (device == RSGPU_ALL_DEVICES) {
+        // every visible gfx950 device; none: a single-device context on
+        // device 0 whose compute calls return RSGPU_ERR_NO_DEVICE
+        std::vector<int> devs;
+        for (int d = 0; d < rsgpu_device_count(); ++d)
+            if (rsgpu_device_ok(d)) devs.push_back(d);
+        if (!devs.empty()) return rsgpu_create_multi(data_shards, parity_shards, devs.data(), (int)devs.size(), flags, out);
+        device = 0;
+    }
     if (device < 0) return RSGPU_ERR_INVALID_ARG;
     std::unique_ptr<rsgpu_ctx> c(new (std::nothrow) rsgpu_ctx());
     if (!c) return RSGPU_ERR_NOMEM;
@@ -526,9 +557,44 @@ int rsgpu_create(int data_shards, int parity_shards, int device, unsigned flags,
     return RSGPU_OK;
 }
 
+int rsgpu_create_multi(int data_shards, int parity_shards, const int *devices, int ndev, unsigned flags,
+                       rsgpu_ctx **out) {
+    if (!out) return RSGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!devices || ndev <= 0) return RSGPU_ERR_INVALID_ARG;
+    rsgpu_ctx *parent = nullptr;
+    int e = rsgpu_create(data_shards, parity_shards, devices[0] < 0 ? -2 : devices[0], flags, &parent);
+    if (e) return e;
+    std::unique_ptr<rsgpu_ctx> P(parent);
+    for (int i = 0; i < ndev; ++i) {
+        for (int j = 0; j < i; ++j)
+            if (devices[j] == devices[i]) return RSGPU_ERR_INVALID_ARG;
+        rsgpu_ctx *c = nullptr;
+        if ((e = rsgpu_create(data_shards, parity_shards, devices[i] < 0 ? -2 : devices[i], flags, &c))) return e;
+        P->subs.emplace_back(c);
+    }
+    *out = P.release();
+    return RSGPU_OK;
+}
+
+int rsgpu_devices(const rsgpu_ctx *ctx, int *out, int cap) {
+    if (!ctx || cap < 0 || (cap > 0 && !out)) return RSGPU_ERR_INVALID_ARG;
+    if (!ctx->multi()) {
+        if (cap > 0) out[0] = ctx->device;
+        return 1;
+    }
+    for (int i = 0; i < (int)ctx->subs.size() && i < cap; ++i) out[i] = ctx->subs[i]->device;
+    return (int)ctx->subs.size();
+}
+
 void rsgpu_destroy(rsgpu_ctx *ctx) {
     if (!ctx) return;
-    if (ctx->dev_state == 1) (void)hipSetDevice(ctx->device);
+    for (auto &c : ctx->subs) rsgpu_destroy(c.release());  // each on its own device
+    DeviceGuard g;  // frees its device memory on its device, then restores the caller's
+    int cur = -1;
+    if (ctx->dev_state == 1 && hipGetDevice(&cur) == hipSuccess && cur != ctx->device &&
+        hipSetDevice(ctx->device) == hipSuccess)
+        g.prev = cur;
     delete ctx;
 }
 
@@ -542,12 +608,14 @@ int rsgpu_matrix(const rsgpu_ctx *ctx, uint8_t *out) {
 }
 
 int rsgpu_encode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards) {
+    RSGPU_FORWARD_RR(rsgpu_encode, shards, lens, nshards);
     if (!ctx || !shards || !lens) return RSGPU_ERR_INVALID_ARG;
     if (nshards != ctx->n) return RSGPU_ERR_TOO_FEW_SHARDS;
     size_t size;
     int e = check_shards(lens, nshards, false, &size);
     if (e) return e;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     auto plan = ctx->plan_encode();
     std::vector<const uint8_t *> in(shards, shards + ctx->k);
     std::vector<uint8_t *> out(shards + ctx->k, shards + ctx->n);
@@ -555,13 +623,15 @@ int rsgpu_encode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
 }
 
 int rsgpu_encode_verify(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
+    RSGPU_FORWARD_RR(rsgpu_encode_verify, shards, lens, nshards, ok);
     if (!ctx || !shards || !lens || !ok) return RSGPU_ERR_INVALID_ARG;
     *ok = 0;
     if (nshards != ctx->n) return RSGPU_ERR_TOO_FEW_SHARDS;
     size_t size;
     int e = check_shards(lens, nshards, false, &size);
     if (e) return e;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     auto enc = ctx->plan_encode();
     auto ver = ctx->plan_verify();
     std::vector<const uint8_t *> in(shards, shards + ctx->k);
@@ -574,13 +644,15 @@ int rsgpu_encode_verify(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *le
 }
 
 int rsgpu_verify(rsgpu_ctx *ctx, const uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
+    RSGPU_FORWARD_RR(rsgpu_verify, shards, lens, nshards, ok);
     if (!ctx || !shards || !lens || !ok) return RSGPU_ERR_INVALID_ARG;
     *ok = 0;
     if (nshards != ctx->n) return RSGPU_ERR_TOO_FEW_SHARDS;
     size_t size;
     int e = check_shards(lens, nshards, false, &size);
     if (e) return e;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     auto plan = ctx->plan_verify();
     std::vector<const uint8_t *> in(shards, shards + ctx->n);
     uint32_t bad = 1;
@@ -609,7 +681,8 @@ static int reconstruct_common(rsgpu_ctx *ctx, uint8_t *const *shards, const size
     if ((e = ctx->plan_reconstruct(present.data(), data_only, check, plan))) return e;
     for (int r = 0; r < plan->nw; ++r)
         if (!shards[plan->out_rows[r]]) return RSGPU_ERR_INVALID_ARG;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     std::vector<const uint8_t *> in;
     for (int row : plan->in_rows) in.push_back(shards[row]);
     std::vector<uint8_t *> out;
@@ -623,10 +696,12 @@ static int reconstruct_common(rsgpu_ctx *ctx, uint8_t *const *shards, const size
 
 int rsgpu_reconstruct(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
                       int data_only) {
+    RSGPU_FORWARD_RR(rsgpu_reconstruct, shards, lens, nshards, data_only);
     return reconstruct_common(ctx, shards, lens, nshards, data_only != 0, false, nullptr);
 }
 
 int rsgpu_decode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards, int *ok) {
+    RSGPU_FORWARD_RR(rsgpu_decode, shards, lens, nshards, ok);
     if (!ok) return RSGPU_ERR_INVALID_ARG;
     *ok = 0;
     return reconstruct_common(ctx, shards, lens, nshards, false, true, ok);
@@ -634,6 +709,7 @@ int rsgpu_decode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
 
 int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
                  const uint8_t *const *newdata, const size_t *new_lens, int nnew) {
+    RSGPU_FORWARD_RR(rsgpu_update, shards, lens, nshards, newdata, new_lens, nnew);
     if (!ctx || !shards || !lens || !newdata || !new_lens) return RSGPU_ERR_INVALID_ARG;
     const int k = ctx->k, n = ctx->n;
     if (nshards != n) return RSGPU_ERR_TOO_FEW_SHARDS;
@@ -651,7 +727,8 @@ int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
     for (int c = 0; c < k; ++c)
         if (new_lens[c]) changed.push_back(c);
     if (changed.empty()) return RSGPU_OK;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     // staging rows: [0,n) shards, [n, n+k) new data, [n+k, n+k+|C|+p) outputs
     const int nc = (int)changed.size();
     Plan plan;
@@ -685,10 +762,12 @@ int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
 
 int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitch,
                      size_t obj_stride, int nobj, void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_encode_dev, d_base, d_base, shard_len, pitch, obj_stride, nobj, stream)
     if (!ctx) return RSGPU_ERR_INVALID_ARG;
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     auto plan = ctx->plan_encode();
     Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
     HIP_TRY(launch_plan(*plan, L, nullptr, (hipStream_t)stream));
@@ -697,10 +776,12 @@ int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitc
 
 int rsgpu_verify_dev(rsgpu_ctx *ctx, const void *d_base, size_t shard_len, size_t pitch,
                      size_t obj_stride, int nobj, uint32_t *d_bad, void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_verify_dev, d_base, d_base, shard_len, pitch, obj_stride, nobj, d_bad, stream)
     if (!ctx || !d_bad) return RSGPU_ERR_INVALID_ARG;
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     auto plan = ctx->plan_verify();
     Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
     HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
@@ -717,7 +798,8 @@ static int recon_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_
     int np = 0;
     for (int i = 0; i < ctx->n; ++i) np += present[i] != 0;
     if (np < ctx->k) return RSGPU_ERR_TOO_FEW_SHARDS;
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     if (np == ctx->n) {
         if (!check) return RSGPU_OK;
         return rsgpu_verify_dev(ctx, d_base, shard_len, pitch, obj_stride, nobj, d_bad, stream);
@@ -816,7 +898,8 @@ static int recon_dev_multi_atlas(rsgpu_ctx *ctx, void *d_base, const uint8_t *pr
         if (slot == kPatSingular) return RSGPU_ERR_SINGULAR;
         hm[o] = mask;
     }
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     AtlasView A;
     if ((e = ctx->atlas_view(mode, A))) return e;
     const unsigned si = ws.next++ % MultiWorkspace::kRing;
@@ -905,7 +988,8 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
         }
         plan_of[o] = *slot_idx;
     }
-    if ((e = ctx->use_device())) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
     if (check && any_checks)
         HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
     Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
@@ -917,12 +1001,16 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
 int rsgpu_reconstruct_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
                                 size_t shard_len, size_t pitch, size_t obj_stride, int nobj,
                                 int data_only, void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_reconstruct_dev_multi, d_base, d_base, present, shard_len, pitch, obj_stride, nobj,
+                      data_only, stream)
     return recon_dev_multi(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, data_only != 0,
                            false, nullptr, stream);
 }
 
 int rsgpu_decode_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                            size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_decode_dev_multi, d_base, d_base, present, shard_len, pitch, obj_stride, nobj, d_bad,
+                      stream)
     if (!d_bad) return RSGPU_ERR_INVALID_ARG;
     return recon_dev_multi(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, false, true, d_bad,
                            stream);
@@ -930,24 +1018,31 @@ int rsgpu_decode_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
 
 int rsgpu_decode_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len,
                            size_t pitch, size_t obj_stride, int nobj, uint32_t *d_status, void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_decode_dev_masks, d_base, d_base, d_masks, shard_len, pitch, obj_stride, nobj, d_status,
+                      stream)
     return dev_masks(ctx, d_base, d_masks, shard_len, pitch, obj_stride, nobj, kAtlasDecode, d_status, stream);
 }
 
 int rsgpu_reconstruct_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len,
                                 size_t pitch, size_t obj_stride, int nobj, int data_only, uint32_t *d_status,
                                 void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_reconstruct_dev_masks, d_base, d_base, d_masks, shard_len, pitch, obj_stride, nobj,
+                      data_only, d_status, stream)
     return dev_masks(ctx, d_base, d_masks, shard_len, pitch, obj_stride, nobj,
                      data_only ? kAtlasData : kAtlasReconstruct, d_status, stream);
 }
 
 int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                           size_t pitch, size_t obj_stride, int nobj, int data_only, void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_reconstruct_dev, d_base, d_base, present, shard_len, pitch, obj_stride, nobj, data_only,
+                      stream)
     return recon_dev(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, data_only != 0, false,
                      nullptr, stream);
 }
 
 int rsgpu_decode_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,
                      size_t pitch, size_t obj_stride, int nobj, uint32_t *d_bad, void *stream) {
+    RSGPU_FORWARD_DEV(rsgpu_decode_dev, d_base, d_base, present, shard_len, pitch, obj_stride, nobj, d_bad, stream)
     if (!d_bad) return RSGPU_ERR_INVALID_ARG;
     return recon_dev(ctx, d_base, present, shard_len, pitch, obj_stride, nobj, false, true, d_bad,
                      stream);

@@ -132,6 +132,10 @@ def _as_u8(buf, writable: bool) -> Optional[np.ndarray]:
         return None
     if isinstance(buf, np.ndarray):
         a = buf
+        if not a.flags.c_contiguous and writable and a.size:
+            # reshape would copy: the device would write into a temporary and
+            # the caller's buffer would silently keep its old bytes
+            raise InvalidArgument("output shard buffer is not contiguous")
         if a.dtype != np.uint8 or a.ndim != 1 or not a.flags.c_contiguous:
             a = a.reshape(-1).view(np.uint8)
     else:
@@ -187,12 +191,20 @@ class RSEncoder:
     """reedsolomon.Encoder backed by the gfx950 kernels (reedsolomon.New)."""
 
     def __init__(self, data_shards: int, parity_shards: int, *, device: int = 0,
-                 matrix: str = "vandermonde", max_goroutines: int = 0):
+                 matrix: str = "vandermonde", max_goroutines: int = 0, devices=None):
+        """device: one GPU, or ALL_DEVICES (-1) for every visible gfx950
+        device; devices: an explicit list (one context over several GPUs,
+        rsgpu_create_multi: objects never cross GPUs)."""
         L = _lib.load()
         self._L = L
         ctx = ctypes.c_void_p()
-        _check(L.rsgpu_create(data_shards, parity_shards, device, MATRIX_KINDS[matrix],
-                              ctypes.byref(ctx)))
+        if devices is not None:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            _check(L.rsgpu_create_multi(data_shards, parity_shards, devs, len(devices),
+                                        MATRIX_KINDS[matrix], ctypes.byref(ctx)))
+        else:
+            _check(L.rsgpu_create(data_shards, parity_shards, device, MATRIX_KINDS[matrix],
+                                  ctypes.byref(ctx)))
         self._ctx = ctx
         self.DataShards = data_shards
         self.ParityShards = parity_shards
@@ -206,6 +218,13 @@ class RSEncoder:
         if ctx:
             self._L.rsgpu_destroy(ctx)
             self._ctx = None
+
+    def devices(self) -> List[int]:
+        """The GPUs this encoder codes on."""
+        n = self._L.rsgpu_devices(self._ctx, None, 0)
+        out = (ctypes.c_int * max(n, 1))()
+        self._L.rsgpu_devices(self._ctx, out, n)
+        return list(out[:n])
 
     def matrix(self) -> np.ndarray:
         out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
@@ -464,11 +483,15 @@ def _join(k: int, dst, shards: Sequence, outSize: int) -> None:
         write -= len(s)
 
 
+ALL_DEVICES = -1  # rsgpu.h RSGPU_ALL_DEVICES
+
+
 def New(dataShards: int, parityShards: int, *, device: int = 0, matrix: str = "vandermonde",
-        max_goroutines: int = 0) -> RSEncoder:
-    """reedsolomon.New: raises ErrInvShardNum / ErrMaxShardNum."""
+        max_goroutines: int = 0, devices=None) -> RSEncoder:
+    """reedsolomon.New: raises ErrInvShardNum / ErrMaxShardNum.  device =
+    ALL_DEVICES or devices=[...] spans several GPUs (RSEncoder)."""
     return RSEncoder(dataShards, parityShards, device=device, matrix=matrix,
-                     max_goroutines=max_goroutines)
+                     max_goroutines=max_goroutines, devices=devices)
 
 
 class DummyEncoder:
@@ -517,10 +540,12 @@ class DummyEncoder:
         _join(self.DataShards, dst, shards, outSize)
 
 
-def NewEncoder(dataShards: int, parityShards: int, ecMaxGoroutine: int, *, device: int = 0):
+def NewEncoder(dataShards: int, parityShards: int, ecMaxGoroutine: int, *, device: int = ALL_DEVICES):
     """client.NewEncoder (/root/reference/client/ec.go:14-24): p == 0 ->
     DummyEncoder; otherwise New(...), printing and swallowing the error (the
-    Go factory then returns a nil Encoder, here None)."""
+    Go factory then returns a nil Encoder, here None).  By default the
+    encoder spans every visible GPU (concurrent EcSet/EcGet calls go to them
+    round-robin), as the Go shim's NewEncoder does."""
     if parityShards == 0:
         return DummyEncoder(dataShards)
     try:

@@ -165,3 +165,37 @@ def test_mixed_pattern_planning_without_device(k, p):
         m[where, :] = 0
         m[where, rng.choice(n, k - 1, replace=False)] = 0x80  # k-1 present
         assert call(m) == oracle.ERR_TOO_FEW_SHARDS, where
+
+
+def test_multi_device_context_host_side():
+    """rsgpu_create_multi / RSGPU_ALL_DEVICES need no device to be created
+    (the matrix is host work); duplicates are rejected; compute calls without
+    a device fail loudly with ErrNoDevice, never on a CPU fallback."""
+    L = _lib.load()
+    ctx = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert L.rsgpu_create_multi(10, 2, devs, 2, 0, ctypes.byref(ctx)) == -20  # duplicate device
+    assert not ctx.value
+    assert L.rsgpu_create_multi(0, 2, devs, 1, 0, ctypes.byref(ctx)) == oracle.ERR_INV_SHARD_NUM
+    enc = ia.New(10, 2, devices=[0])
+    assert enc.devices() == [0]
+    assert np.array_equal(enc.matrix(), ia.New(10, 2).matrix())
+    allenc = ia.New(10, 2, device=ia.ALL_DEVICES)
+    assert len(allenc.devices()) >= 1
+    if not ia.device_ok(0):
+        sh = [np.zeros(8, np.uint8) for _ in range(12)]
+        with pytest.raises(ia.NoDevice):
+            enc.Encode(sh)
+        with pytest.raises(ia.NoDevice):
+            allenc.Encode(sh)
+
+
+def test_noncontiguous_output_buffer_rejected():
+    """An output shard that is a strided view would be copied by the host
+    mirror, the device writing into the copy: refused before any device work."""
+    enc = ia.New(4, 2)
+    big = np.zeros((6, 32), np.uint8)
+    sh = [big[i] for i in range(4)] + [big[4, ::2], big[5, ::2]]  # strided parity rows
+    sh = [s if i >= 4 else s[:16] for i, s in enumerate(sh)]
+    with pytest.raises(ia.InvalidArgument):
+        enc.Encode(sh)

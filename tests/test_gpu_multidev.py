@@ -1,0 +1,191 @@
+"""Multi-device contexts, the host pipeline at config-5 sizes, and the
+host-memory edge cases, through the C ABI against the oracle (bit-exact).
+
+* A context over every visible GPU (RSGPU_ALL_DEVICES / rsgpu_create_multi,
+  what the Go shim's NewEncoder builds, client/ec.go:14-24): per-object
+  calls round-robin, batch calls split objects o -> device o mod N,
+  device-resident calls follow the memory.  The test box has one GPU, so
+  these run the forwarding path with N = 1; the driver's 8-GPU node runs the
+  same code with N = 8.
+* BASELINE config 5's host pipeline at its real sizes: a log-uniform trace
+  with 4 KiB objects and a 64+ MiB object (client/ecRedis.go:96 Set buffer,
+  :161-173 gathered Get buffers), pinned and pageable.
+* Pinned user memory (rsgpu_host_register, no slack past the buffer) with a
+  shard size that is not a multiple of 16."""
+import numpy as np
+import pytest
+
+import infinicache_amd as ia
+import oracle
+from oracle import rs_numpy as rn
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+SEED = 0x1F1C
+
+
+def _full(k, p, size, idx):
+    d = rn.splitmix64_bytes(SEED, idx, k * size).reshape(k, size)
+    e, sh = oracle.encode(k, p, [d[i] for i in range(k)] + [bytes(size)] * p)
+    assert e == 0
+    return sh
+
+
+def test_all_devices_context(gpu):
+    enc = ia.New(10, 2, device=ia.ALL_DEVICES)
+    assert enc.devices() == [d for d in range(ia.device_count()) if ia.device_ok(d)]
+    # per-object calls round-robin over the devices: Client.encode / decode
+    for i, size in enumerate([1, 103, 4096, 104858, 77777]):
+        full = _full(10, 2, size, 900 + i)
+        sh = [full[j].copy() if j < 10 else np.zeros(size, np.uint8) for j in range(12)]
+        assert enc.EncodeVerify(sh)
+        for j in range(12):
+            assert np.array_equal(sh[j], full[j]), (size, j)
+        got = [None if j in (i % 12, (i + 5) % 12) else sh[j] for j in range(12)]
+        assert enc.DecodeVerify(got)
+        for j in range(12):
+            assert np.array_equal(got[j], full[j]), (size, j)
+
+
+def test_multi_device_batches(gpu):
+    devs = [d for d in range(ia.device_count()) if ia.device_ok(d)]
+    enc = ia.New(10, 4, devices=devs)
+    sizes = [5, 4096, 1 << 20, 333, 70001, 4 << 20, 17]
+    objs, fulls = [], []
+    for i, nb in enumerate(sizes):
+        data = rn.splitmix64_bytes(SEED, 950 + i, nb)
+        sh = enc.Split(data)
+        S = len(sh[0])
+        buf = ia.host_alloc(14 * S) if i % 2 else np.zeros(14 * S, np.uint8)
+        buf[:] = np.concatenate(sh)
+        objs.append([buf[j * S:(j + 1) * S] for j in range(14)])
+        e, want = oracle.encode(10, 4, [s.copy() for s in sh[:10]] + [bytes(S)] * 4)
+        fulls.append(want)
+    enc.encode_batch(objs)
+    for sh, want in zip(objs, fulls):
+        for j in range(14):
+            assert np.array_equal(sh[j], want[j])
+    lost = [(0, 5), (1, 2, 3), (), (13,), (0, 10, 11, 12), (6, 7), (9,)]
+    present = [[j not in lost[o] for j in range(14)] for o in range(len(sizes))]
+    for o in range(len(sizes)):
+        for j in lost[o]:
+            objs[o][j][:] = 0xEE
+    ok = enc.decode_batch(objs, present=present)
+    assert ok == [True] * len(sizes)
+    for sh, want in zip(objs, fulls):
+        for j in range(14):
+            assert np.array_equal(sh[j], want[j])
+
+
+def test_multi_device_dev_calls_follow_the_memory(gpu):
+    enc = ia.New(10, 2, device=ia.ALL_DEVICES)
+    k, p, S, nobj = 10, 2, 5000, 6
+    pitch = 5120
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    b = torch.randint(0, 256, (nobj, k + p, pitch), dtype=torch.uint8, device="cuda:0", generator=g)
+    b[:, :, S:] = 0
+    enc.encode_dev(b, S, pitch, (k + p) * pitch, nobj, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    h = b.cpu().numpy()
+    m = enc.matrix()
+    for o in range(nobj):
+        want = oracle.apply(m[k:], [h[o, c, :S] for c in range(k)])
+        for r in range(p):
+            assert np.array_equal(h[o, k + r, :S], want[r])
+    hostbuf = np.zeros((k + p) * pitch, np.uint8)  # not device memory: no device owns it
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev(hostbuf.ctypes.data, S, pitch, (k + p) * pitch, 1)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_trace_pipeline_config5_sizes(gpu, pinned):
+    """encode_batch + decode_batch over a small log-uniform trace: 4 KiB
+    objects beside one 64+ MiB object (S > 6.7 MB), against the oracle."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    rng = np.random.Generator(np.random.PCG64(20200225))
+    sizes = [4096, 4096 + 7] + [int(x) for x in np.exp(rng.uniform(np.log(4096), np.log(1 << 20), 4))]
+    sizes += [(64 << 20) + 12345]
+    objs, wants = [], []
+    for i, nb in enumerate(sizes):
+        S = (nb + k - 1) // k
+        buf = ia.host_alloc(n * S) if pinned else np.empty(n * S, np.uint8)
+        buf[:nb] = rn.splitmix64_bytes(SEED, 1000 + i, nb)
+        buf[nb:] = 0
+        sh = [buf[j * S:(j + 1) * S] for j in range(n)]
+        want = oracle.code_fast(enc.matrix()[k:], [sh[j] for j in range(k)], nthreads=16)
+        objs.append(sh)
+        wants.append(want)
+    enc.encode_batch(objs)
+    for sh, want in zip(objs, wants):
+        for r in range(p):
+            assert np.array_equal(sh[k + r], want[r])
+    golden = [[sh[j].copy() for j in range(n)] for sh in objs]
+    lost = (0, 5)
+    for sh in objs:
+        for j in lost:
+            sh[j][:] = 0
+    ok = enc.decode_batch(objs, present=[[j not in lost for j in range(n)]] * len(objs))
+    assert all(ok)
+    for sh, gd in zip(objs, golden):
+        for j in range(n):
+            assert np.array_equal(sh[j], gd[j])
+
+
+@pytest.mark.parametrize("S", [1003, 4097, 104858])
+def test_registered_user_buffer_unaligned_shards(gpu, S):
+    """A numpy Split buffer pinned with rsgpu_host_register (no slack: the
+    last row's 16-B vector would run past the end, so the pass must not read
+    it in place) and unregistered afterwards."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    full = _full(k, p, S, 1100 + S % 97)
+    buf = np.empty(n * S, np.uint8)
+    ia.host_register(buf)
+    try:
+        for j in range(n):
+            buf[j * S:(j + 1) * S] = full[j] if j < k else 0
+        sh = [buf[j * S:(j + 1) * S] for j in range(n)]
+        enc.Encode(sh)
+        for j in range(n):
+            assert np.array_equal(sh[j], full[j])
+        assert enc.Verify(sh)
+        sh[k][:] = 0
+        assert enc.EncodeVerify(sh)
+        assert np.array_equal(sh[k], full[k])
+        got = [None if j in (0, n - 1) else sh[j] for j in range(n)]
+        enc.Reconstruct(got)
+        for j in range(n):
+            assert np.array_equal(got[j], full[j])
+    finally:
+        ia.host_unregister(buf)
+
+
+def test_pass_image_cache_keyed_by_shard_len(gpu):
+    """A wide code (n > 16: host-planned mixed-pattern path) decoded twice on
+    one encoder, same pitch, two shard lengths: the cached pass images must
+    not carry the first call's span into the second."""
+    k, p = 20, 4
+    n = k + p
+    enc = ia.New(k, p)
+    pitch = 8192
+    s = torch.cuda.current_stream()
+    for S, seed in ((1000, 1), (8000, 2)):
+        nobj = 5
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        b = torch.randint(0, 256, (nobj, n, pitch), dtype=torch.uint8, device="cuda", generator=g)
+        b[:, :, S:] = 0
+        enc.encode_dev(b, S, pitch, n * pitch, nobj, s)
+        golden = b.clone()
+        present = np.ones((nobj, n), np.uint8)
+        for o in range(nobj):
+            present[o, [o, o + 7]] = 0
+            b[o, o] = 0
+            b[o, o + 7] = 0
+        bad = torch.full((nobj,), 3, dtype=torch.int32, device="cuda")
+        enc.decode_dev_multi(b, present, S, pitch, n * pitch, nobj, bad, s)
+        torch.cuda.synchronize()
+        assert not bad.any()
+        assert torch.equal(b[:, :, :S], golden[:, :, :S]), S
