@@ -140,6 +140,22 @@ int rsgpu_decode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
 int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
                  const uint8_t *const *newdata, const size_t *new_lens, int nnew);
 
+/* ---- per-object calls on one contiguous image ----------------------------
+ * Shard i of the object is base[i*shard_len, (i+1)*shard_len): Split's layout
+ * (ecRedis.go:384 — Split returns consecutive slices of one backing array).
+ * One pointer crosses the boundary, so a cgo caller passes the Split backing
+ * array itself (Go memory holding no Go pointers: legal under cgo's rules), or
+ * a C-owned pinned image it copied gathered shards into (EcGet's separate
+ * buffers, ecRedis.go:161-170).  present: bit i set = shard i holds data
+ * (the others are missing and get written); data+parity <= 64.  Semantics,
+ * checks and errors are those of the pointer-table calls above. */
+int rsgpu_encode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards);
+int rsgpu_encode_verify_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards, int *ok);
+int rsgpu_verify_image(rsgpu_ctx *ctx, const uint8_t *base, size_t shard_len, int nshards, int *ok);
+int rsgpu_reconstruct_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards, uint64_t present,
+                            int data_only);
+int rsgpu_decode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards, uint64_t present, int *ok);
+
 /* ---- batched device-resident API (HBM in, HBM out) ---------------------
  * Layout: shard i of object o lives at d_base + o*obj_stride + i*pitch, for
  * i in [0, data+parity).  Requirements: d_base and obj_stride 16-B aligned,

@@ -23,7 +23,8 @@ EXPORTS = (
     "rsgpu_decode_dev_multi", "rsgpu_encode_batch", "rsgpu_decode_batch",
     "rsgpu_host_register", "rsgpu_host_unregister", "rsgpu_host_alloc", "rsgpu_host_free",
     "rsgpu_encode_verify", "rsgpu_decode_dev_masks", "rsgpu_reconstruct_dev_masks",
-    "rsgpu_create_multi", "rsgpu_devices",
+    "rsgpu_create_multi", "rsgpu_devices", "rsgpu_encode_image", "rsgpu_encode_verify_image",
+    "rsgpu_verify_image", "rsgpu_reconstruct_image", "rsgpu_decode_image",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -87,6 +88,11 @@ def load():
     L.rsgpu_decode_dev_multi.argtypes = [vp, vp, u8p, sz, sz, sz, ci, vp, vp]
     L.rsgpu_decode_dev_masks.argtypes = [vp, vp, vp, sz, sz, sz, ci, vp, vp]
     L.rsgpu_reconstruct_dev_masks.argtypes = [vp, vp, vp, sz, sz, sz, ci, ci, vp, vp]
+    L.rsgpu_encode_image.argtypes = [vp, vp, sz, ci]
+    L.rsgpu_encode_verify_image.argtypes = [vp, vp, sz, ci, intp]
+    L.rsgpu_verify_image.argtypes = [vp, vp, sz, ci, intp]
+    L.rsgpu_reconstruct_image.argtypes = [vp, vp, sz, ci, ctypes.c_uint64, ci]
+    L.rsgpu_decode_image.argtypes = [vp, vp, sz, ci, ctypes.c_uint64, intp]
     L.rsgpu_encode_batch.argtypes = [vp, u8pp, szp, ci]
     L.rsgpu_decode_batch.argtypes = [vp, u8pp, u8p, szp, ci, intp]
     L.rsgpu_host_register.argtypes = [vp, sz]

@@ -758,6 +758,67 @@ int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
     return run_host(ctx, plan, n + k + nc + ctx->p, size, in, out, nullptr);
 }
 
+// ------------------------------------------- contiguous-image host calls
+// Thin forms of the pointer-table calls for Split's contiguous layout: the
+// table is built here, on the C side, so a cgo caller passes one pointer.
+
+namespace {
+
+int image_table(const rsgpu_ctx *ctx, const uint8_t *base, size_t shard_len, int nshards, uint64_t present,
+                std::vector<uint8_t *> &ptrs, std::vector<size_t> &lens) {
+    if (!ctx || !base) return RSGPU_ERR_INVALID_ARG;
+    if (nshards <= 0 || nshards > 64) return nshards != ctx->n ? RSGPU_ERR_TOO_FEW_SHARDS : RSGPU_ERR_INVALID_ARG;
+    ptrs.resize(nshards);
+    lens.resize(nshards);
+    for (int i = 0; i < nshards; ++i) {
+        ptrs[i] = const_cast<uint8_t *>(base) + (size_t)i * shard_len;
+        lens[i] = (present >> i) & 1 ? shard_len : 0;
+    }
+    return RSGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsgpu_encode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards) {
+    std::vector<uint8_t *> p;
+    std::vector<size_t> l;
+    int e = image_table(ctx, base, shard_len, nshards, ~0ull, p, l);
+    return e ? e : rsgpu_encode(ctx, p.data(), l.data(), nshards);
+}
+
+int rsgpu_encode_verify_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards, int *ok) {
+    std::vector<uint8_t *> p;
+    std::vector<size_t> l;
+    int e = image_table(ctx, base, shard_len, nshards, ~0ull, p, l);
+    return e ? e : rsgpu_encode_verify(ctx, p.data(), l.data(), nshards, ok);
+}
+
+int rsgpu_verify_image(rsgpu_ctx *ctx, const uint8_t *base, size_t shard_len, int nshards, int *ok) {
+    std::vector<uint8_t *> p;
+    std::vector<size_t> l;
+    int e = image_table(ctx, base, shard_len, nshards, ~0ull, p, l);
+    return e ? e : rsgpu_verify(ctx, (const uint8_t *const *)p.data(), l.data(), nshards, ok);
+}
+
+int rsgpu_reconstruct_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards, uint64_t present,
+                            int data_only) {
+    std::vector<uint8_t *> p;
+    std::vector<size_t> l;
+    int e = image_table(ctx, base, shard_len, nshards, present, p, l);
+    return e ? e : rsgpu_reconstruct(ctx, p.data(), l.data(), nshards, data_only);
+}
+
+int rsgpu_decode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nshards, uint64_t present, int *ok) {
+    std::vector<uint8_t *> p;
+    std::vector<size_t> l;
+    int e = image_table(ctx, base, shard_len, nshards, present, p, l);
+    return e ? e : rsgpu_decode(ctx, p.data(), l.data(), nshards, ok);
+}
+
+}  // extern "C"
+
 // ---------------------------------------------------- device-resident API
 
 int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitch,

@@ -58,6 +58,15 @@ static int host_checks(void) {
     for (int i = 0; i < 12; i++) lens[i] = i < 9 ? 8 : 0;
     CHECK(rsgpu_reconstruct(ctx, sh, lens, 12, 0) == RSGPU_ERR_TOO_FEW_SHARDS);
     CHECK(strlen(rsgpu_strerror(RSGPU_ERR_SHARD_SIZE)) > 0);
+    /* the image calls: one base pointer, same checks */
+    CHECK(rsgpu_encode_image(ctx, a, 8, 11) == RSGPU_ERR_TOO_FEW_SHARDS);
+    CHECK(rsgpu_encode_image(ctx, NULL, 8, 12) == RSGPU_ERR_INVALID_ARG);
+    CHECK(rsgpu_reconstruct_image(ctx, a, 8, 12, 0x1ff, 0) == RSGPU_ERR_TOO_FEW_SHARDS);
+    CHECK(rsgpu_encode_image(ctx, a, 0, 12) == RSGPU_ERR_SHARD_NO_DATA);
+    rsgpu_destroy(ctx);
+    int devs[2] = {0, 0};
+    CHECK(rsgpu_create_multi(10, 2, devs, 2, 0, &ctx) == RSGPU_ERR_INVALID_ARG && ctx == NULL);
+    CHECK(rsgpu_create(10, 2, RSGPU_ALL_DEVICES, 0, &ctx) == RSGPU_OK && rsgpu_devices(ctx, devs, 2) >= 1);
     rsgpu_destroy(ctx);
     printf("host checks ok (devices: %d)\n", rsgpu_device_count());
     return 0;
@@ -134,8 +143,121 @@ static int gpu_checks(void) {
     return 0;
 }
 
+/* ecredis_replay: client/ecRedis.go:382-432 in its exact call order, through
+ * the routes the Go shim (integration/go/client/ec_gpu.go) takes so that only
+ * cgo-legal pointers cross:
+ *   Client.encode: Split into ONE contiguous array (route i: the *_image
+ *   calls take its base), Encode, Verify (false -> error).
+ *   Client.decode over EcGet's 12 separate buffers, 2 of them nil (the
+ *   proxy's first-d rule): Verify -> (false, ErrShardSize) with no device
+ *   work (:406; the shim answers it in Go); Reconstruct through a C-owned
+ *   pinned image (route ii), rebuilt shards copied out; Verify -> true, which
+ *   upstream stores in stats.Corrupted (true on SUCCESS, :420-426); Join.
+ *   Then a Get whose extra present parity shard is corrupted: Reconstruct
+ *   succeeds, the second Verify is false -> decode's error path.  The fused
+ *   forms (rsgpu_encode_verify_image, rsgpu_decode_image) give the same
+ *   booleans and bytes. */
+static int ecredis_replay(void) {
+    const int k = 10, p = 2, n = 12;
+    const size_t N = 1 << 20, S = (N + k - 1) / k;
+    rsgpu_ctx *ctx;
+    CHECK(rsgpu_create(k, p, RSGPU_ALL_DEVICES, 0, &ctx) == RSGPU_OK);
+    uint8_t *obj = malloc(N);
+    for (size_t j = 0; j < N; j++) obj[j] = rnd8();
+    /* ---- Client.encode (ecRedis.go:382-402) */
+    uint8_t *split = calloc(n, S); /* Split: perShard = ceil(N/k), zero pad */
+    memcpy(split, obj, N);
+    CHECK(rsgpu_encode_image(ctx, split, S, n) == RSGPU_OK);
+    int ok = 0;
+    CHECK(rsgpu_verify_image(ctx, split, S, n, &ok) == RSGPU_OK && ok == 1);
+    uint8_t *ref[12];
+    size_t lens[12];
+    for (int i = 0; i < n; i++) {
+        ref[i] = malloc(S);
+        memcpy(ref[i], split + i * S, S);
+        lens[i] = S;
+    }
+    for (int i = k; i < n; i++) memset(ref[i], 0, S);
+    CHECK(orc_encode(k, p, 0, ref, lens, n) == 0);
+    for (int i = k; i < n; i++) CHECK(memcmp(ref[i], split + i * S, S) == 0);
+    uint8_t *split2 = calloc(n, S);
+    memcpy(split2, obj, N);
+    CHECK(rsgpu_encode_verify_image(ctx, split2, S, n, &ok) == RSGPU_OK && ok == 1);
+    CHECK(memcmp(split, split2, n * S) == 0);
+    /* ---- Client.decode (ecRedis.go:404-432): 12 separate Get buffers */
+    for (int trial = 0; trial < 2; trial++) {
+        const int lost[2] = {3, 10};
+        uint8_t *got[12];
+        for (int i = 0; i < n; i++) {
+            got[i] = (i == lost[0] || i == lost[1]) ? NULL : malloc(S);
+            lens[i] = got[i] ? S : 0;
+            if (got[i]) memcpy(got[i], split + i * S, S);
+        }
+        if (trial == 1) {  /* an 11-present Get: shard 10 arrives too; the extra (11) is corrupted */
+            got[10] = malloc(S);
+            memcpy(got[10], split + 10 * S, S);
+            lens[10] = S;
+            got[11][777] ^= 0x20;
+        }
+        /* stats.AllGood, _ = Verify(data): nil shards -> (false, ErrShardSize) */
+        ok = 7;
+        CHECK(rsgpu_verify(ctx, (const uint8_t *const *)got, lens, n, &ok) == RSGPU_ERR_SHARD_SIZE && ok == 0);
+        /* Reconstruct(data): stage the present shards in a C-owned pinned image */
+        uint8_t *img = NULL;
+        CHECK(rsgpu_host_alloc(n * S, (void **)&img) == RSGPU_OK);
+        uint64_t present = 0;
+        for (int i = 0; i < n; i++)
+            if (lens[i]) {
+                memcpy(img + i * S, got[i], S);
+                present |= 1ull << i;
+            }
+        CHECK(rsgpu_reconstruct_image(ctx, img, S, n, present, 0) == RSGPU_OK);
+        for (int i = 0; i < n; i++)
+            if (!lens[i]) {  /* upstream allocates the missing shard */
+                got[i] = malloc(S);
+                memcpy(got[i], img + i * S, S);
+                lens[i] = S;
+            }
+        /* stats.Corrupted, err = Verify(data): true on success (:420) */
+        int corrupted = 0;
+        CHECK(rsgpu_verify(ctx, (const uint8_t *const *)got, lens, n, &corrupted) == RSGPU_OK);
+        if (trial == 0) {
+            CHECK(corrupted == 1);
+            /* Join: the first N bytes of the data shards */
+            for (int i = 0; i < k; i++) {
+                const size_t off = (size_t)i * S, len = off + S <= N ? S : (off < N ? N - off : 0);
+                CHECK(memcmp(got[i], obj + off, len) == 0);
+            }
+        } else {
+            CHECK(corrupted == 0);  /* decode returns the error */
+        }
+        /* the fused decode gives the same boolean and bytes */
+        uint8_t *img2 = NULL;
+        CHECK(rsgpu_host_alloc(n * S, (void **)&img2) == RSGPU_OK);
+        uint64_t pres2 = 0;
+        for (int i = 0; i < n; i++)
+            if (i != lost[0] && (i != lost[1] || trial == 1)) {
+                memcpy(img2 + i * S, i == 11 && trial == 1 ? got[11] : split + i * S, S);
+                pres2 |= 1ull << i;
+            }
+        int fused_ok = 7;
+        CHECK(rsgpu_decode_image(ctx, img2, S, n, pres2, &fused_ok) == RSGPU_OK);
+        CHECK(fused_ok == corrupted);
+        CHECK(memcmp(img2 + lost[0] * S, split + lost[0] * S, S) == 0);
+        CHECK(rsgpu_host_free(img) == RSGPU_OK && rsgpu_host_free(img2) == RSGPU_OK);
+        for (int i = 0; i < n; i++) free(got[i]);
+    }
+    for (int i = 0; i < n; i++) free(ref[i]);
+    free(split);
+    free(split2);
+    free(obj);
+    rsgpu_destroy(ctx);
+    printf("ecredis replay ok (Client.encode/decode call order, contiguous and staged routes)\n");
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (host_checks()) return 1;
-    if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_checks();
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_checks() || ecredis_replay();
     return 0;
 }

@@ -38,3 +38,4 @@ def test_c_abi_gpu_paths(gpu, client_bin):
     r = subprocess.run([client_bin, "gpu"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr + r.stdout
     assert "gpu checks ok" in r.stdout
+    assert "ecredis replay ok" in r.stdout
