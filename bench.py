@@ -46,6 +46,16 @@ WORKLOADS = {
     "small": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
                   palign=16,
                   desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, device-resident"),
+    # the reference's own example object (client/example/main.go:15,26): 1 KiB,
+    # S = 103; palign: row pitch rounded to 16 (112), 4 (104) or 1 (103,
+    # byte-packed rows; the object stride is n * pitch either way)
+    "small1k": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
+                    palign=16, desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, pitch 112"),
+    "small1k_p4": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
+                       palign=4, desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, pitch 104"),
+    "small1k_p1": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
+                       palign=1, desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, "
+                                      "byte-packed rows (pitch 103)"),
     "small_mixed": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
                         palign=16, mixed=True,
                         desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, per-object "
@@ -73,6 +83,9 @@ METRICS = {
     "encdec_upstream": "RS(10+2) encode+decode GiB/s (device-resident, unfused Reconstruct+Verify Get), 1 MB objects",
     "small": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
     "small_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 4 KiB objects",
+    "small1k": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
+    "small1k_p4": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
+    "small1k_p1": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
     "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
 }
 
@@ -262,7 +275,13 @@ def run_trace(args):
     S = (sizes + k - 1) // k
     offs = np.concatenate([[0], np.cumsum(n * S)])
     total_obj = int(sizes.sum())
-    enc = ia.New(k, p)
+    # --devices N (N > 1): one multi-device context, as the Go shim's
+    # NewEncoder builds it: object o -> GPU o mod N, one pipeline and PCIe
+    # link per GPU, all in this one process
+    ndev = max(1, args.devices)
+    if ndev > torch.cuda.device_count():
+        raise SystemExit(f"--devices {ndev} but {torch.cuda.device_count()} GPU(s) visible")
+    enc = ia.New(k, p, devices=list(range(ndev))) if ndev > 1 else ia.New(k, p)
     host = ia.host_alloc(int(offs[-1]))
     # random object bytes: one 256 MiB device random block, copied around
     rnd = torch.randint(0, 256, (256 << 20,), dtype=torch.uint8, device="cuda").cpu().numpy()
@@ -344,7 +363,7 @@ def run_trace(args):
         "metric": "RS(10+2) encode+decode GiB/s, mixed 4 KiB-100 MiB trace, host<->device copies included",
         "value": round(e2e, 2),
         "unit": "GiB/s",
-        "n_gpus": 1,
+        "n_gpus": ndev,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 2),
@@ -354,7 +373,7 @@ def run_trace(args):
         "dtype": "u8",
         "data": "synthetic: log-uniform sizes (PCG64 seed 20200225), random bytes, pinned host memory",
         "config": {"workload": "config 5 mixed trace, e2e (pinned H2D -> gf_apply -> D2H, 4 slots/streams)",
-                   "objects": nobj, "total_object_bytes": total_obj,
+                   "devices_in_process": ndev, "objects": nobj, "total_object_bytes": total_obj,
                    "size_min": int(sizes.min()), "size_max": int(sizes.max()),
                    "size_median": int(np.median(sizes))},
         "device_resident_same_trace_GiBps": round(dev_rate, 2),
@@ -446,6 +465,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace", "latency"])
     ap.add_argument("--trace-objects", type=int, default=512)
+    ap.add_argument("--devices", type=int, default=1,
+                    help="trace: GPUs driven by ONE process through a multi-device context")
     ap.add_argument("--batch", type=int, default=0, help="objects per GPU (default: workload's)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the workload's batch is the TOTAL, split over ranks")

@@ -158,13 +158,17 @@ int rsgpu_decode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nsha
 
 /* ---- batched device-resident API (HBM in, HBM out) ---------------------
  * Layout: shard i of object o lives at d_base + o*obj_stride + i*pitch, for
- * i in [0, data+parity).  Requirements: d_base and obj_stride 16-B aligned,
- * pitch % 16 == 0, pitch >= shard_len rounded up to 16, and
- * (data+parity-1)*pitch + pitch < 4 GiB.  Kernels read/write whole 16-B
- * vectors, so written rows' bytes in [shard_len, roundup16(shard_len)) are
- * overwritten with the coding of the input rows' pad bytes (zero when those
- * are zero).  `stream` is a hipStream_t (NULL = default stream); calls are
- * asynchronous on it and make no host<->device synchronisation. */
+ * i in [0, data+parity).  Requirements: pitch >= shard_len, obj_stride >=
+ * (data+parity)*pitch when nobj > 1, and (data+parity)*pitch < 4 GiB; any
+ * alignment (16-B aligned d_base, pitch and obj_stride are the fast path and
+ * are required by the *_dev_masks calls).  Kernels read whole 16-B vectors
+ * and write them where the row's pitch allows: written rows' bytes in
+ * [shard_len, min(pitch, roundup16(shard_len))) are overwritten with the
+ * coding of the input rows' pad bytes (zero when those are zero); with a
+ * pitch below roundup16(shard_len) (e.g. pitch = shard_len, byte-packed rows)
+ * nothing past shard_len is written.  `stream` is a hipStream_t (NULL =
+ * default stream); calls are asynchronous on it and make no host<->device
+ * synchronisation. */
 
 /* Encode nobj objects: rows [k, k+p) <- M[k:] x rows [0, k). */
 int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitch,

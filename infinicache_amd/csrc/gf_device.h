@@ -43,25 +43,40 @@ __device__ __forceinline__ uint32_t gf_mac(uint32_t acc, T *t, const GfIdx &g) {
     return acc ^ lut8(t[4], t[4], g.i2);
 }
 
-// Store one 16-B output vector.  With byte-packed rows (pitch = shard size,
-// the host API's staging layout) the last vector of a row overlaps the next
-// row, so its `tail` valid bytes are stored one by one.  Rows need no 16-B
-// alignment: gfx950 buffer loads/stores honour unaligned offsets (the
-// driver's SH_MEM_CONFIG unaligned mode; tools/unaligned_probe.hip).
+// Store one 16-B output vector.  `part` (0..15) is non-zero only for the last
+// vector of a row whose pitch is not a multiple of 16 and leaves fewer than
+// 16 bytes to the next row (the host API's byte-packed staging image, pitch =
+// S; device batches with pitch = S rounded to 4): only the row's first `part`
+// bytes of that vector may be written, as one 8/4/2/1-byte store each.
+// Rows need no 16-B alignment: gfx950 buffer loads/stores honour unaligned
+// offsets (the driver's SH_MEM_CONFIG unaligned mode; tools/unaligned_probe.hip).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <int SAUX>
 __device__ __forceinline__ void store_row(const u32x4 &o, __amdgpu_buffer_rsrc_t rs, uint32_t voff,
-                                          uint32_t soff, bool last_packed, uint32_t tail) {
-    if (last_packed && tail < 16u) {
-        for (uint32_t b = 0; b < tail; ++b) {
-            // select the dword without indexing the vector by a runtime value
-            // (that would put `o` in private memory: a scratch frame per lane)
-            const uint32_t q = b >> 2;
-            const uint32_t w = q == 0 ? o[0] : q == 1 ? o[1] : q == 2 ? o[2] : o[3];
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8 * (b & 3))), rs, voff + b, soff, SAUX);
-        }
-    } else {
+                                          uint32_t soff, uint32_t part) {
+    if (part == 0u) {
         __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, soff, SAUX);
+        return;
     }
+    // select dwords with compares, never by indexing the vector with a
+    // runtime value (that puts `o` in private memory: a scratch frame per lane)
+    uint32_t off = 0;
+    if (part & 8u) {
+        const u32x2 lo = {o[0], o[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(lo, rs, voff, soff, SAUX);
+        off = 8;
+    }
+    if (part & 4u) {
+        __builtin_amdgcn_raw_buffer_store_b32(off ? o[2] : o[0], rs, voff + off, soff, SAUX);
+        off += 4;
+    }
+    uint32_t rem = off == 12 ? o[3] : off == 8 ? o[2] : off == 4 ? o[1] : o[0];
+    if (part & 2u) {
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)rem, rs, voff + off, soff, SAUX);
+        off += 2;
+        rem >>= 16;
+    }
+    if (part & 1u) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)rem, rs, voff + off, soff, SAUX);
 }
 
 // mask of the valid bytes of dword d in a 16-B vector holding `valid` bytes
@@ -79,7 +94,7 @@ struct Pass {
     uint32_t ki;     // trailing identity inputs (see gf_apply_body)
     uint32_t clear;  // the plan has no check rows: this pass zeroes bad[obj]
     uint32_t span;   // bytes addressable from an object base
-    uint32_t packed; // rows are byte-packed (pitch % 16 != 0): see store_row
+    uint32_t packed; // bytes of a row's last vector that may be written when < 16, else 0 (store_row)
     uint32_t in_off[K];
     uint32_t out_off[R];
     uint32_t tab[K * R * kTabWords];  // input-major [K][R][kTabWords]: scalar loads per input
@@ -122,9 +137,21 @@ struct ApplyArgs {  // one pass for every object of the launch (kernarg)
     uint32_t opw;    // objects per workgroup (> 1: small objects, item = group of opw)
     uint32_t nobj;   // objects in the launch (bounds the last group when opw > 1)
     uint32_t gspan;  // opw > 1: bytes a group's objects cover from the first one's base
+    // bytes readable from base: the rows of the launch's last object end here.
+    // A row's last 16-B vector may reach up to 15 bytes past its pitch; the
+    // ranges are clamped to this so the last object never reads past the
+    // caller's buffer (those bytes only feed pad bytes)
+    uint64_t limit;
     Order ord;       // item = object, or group of opw objects
     Pass<K, R> p;
 };
+
+// buffer-range bytes for an object (or group) at offset `at` from the launch
+// base: its span, clamped to the launch's readable limit
+__device__ __forceinline__ uint32_t clamp_span(uint32_t span, uint64_t limit, uint64_t at) {
+    const uint64_t left = limit > at ? limit - at : 0;
+    return left < span ? (uint32_t)left : span;
+}
 
 template <int K, int R>
 struct MultiArgs {  // per-object passes (a Get batch with mixed erasure patterns)
@@ -140,6 +167,7 @@ struct MultiArgs {  // per-object passes (a Get batch with mixed erasure pattern
     // pass, objs[i*opw + j] (~0u: empty slot), passes[obj_pass[i]]; lanes
     // address object o at o * obj_stride from base, within gspan bytes
     uint32_t opw, gspan;
+    uint64_t limit;  // bytes readable from base (see ApplyArgs::limit)
 };
 
 // One workgroup = BS lanes x U vectors of 16 B of one object (grid.y).
@@ -192,7 +220,7 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
             if (rd.copy_in) {
 #pragma unroll
                 for (int c = 0; c < K; ++c)
-                    store_row<SAUX>(x[u][c], rs, lane_off + v * 16u, a.in_off[c], a.packed && v == nvec - 1, tail);
+                    store_row<SAUX>(x[u][c], rs, lane_off + v * 16u, a.in_off[c], v == nvec - 1 ? a.packed : 0u);
             }
         }
     }
@@ -235,8 +263,8 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         for (int r = 0; r < R; ++r) {
             if ((uint32_t)r < a.nw) {
                 u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                store_row<SAUX>(o, rso, lane_off + v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
-                if (rd.dual) store_row<SAUX>(o, rs, lane_off + v * 16u, a.out_off[r], a.packed && v == nvec - 1, tail);
+                store_row<SAUX>(o, rso, lane_off + v * 16u, a.out_off[r], v == nvec - 1 ? a.packed : 0u);
+                if (rd.dual) store_row<SAUX>(o, rs, lane_off + v * 16u, a.out_off[r], v == nvec - 1 ? a.packed : 0u);
             } else {
                 const uint32_t valid = (v == nvec - 1) ? tail : 16u;
 #pragma unroll
@@ -261,7 +289,8 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
         if (j >= a.opw || o0 + j >= a.nobj) return;
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)o0 * a.obj_stride, o0 + j, a.p, a.nvec,
                                                a.tail, a.bad, threadIdx.x - j * a.nvec, Redirect(),
-                                               j * (uint32_t)a.obj_stride, a.gspan);
+                                               j * (uint32_t)a.obj_stride,
+                                               clamp_span(a.gspan, a.limit, (uint64_t)o0 * a.obj_stride));
         return;
     }
     Redirect rd;
@@ -271,7 +300,8 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
     rd.out = a.out_base;
     rd.dual = a.out_dual != 0;
     gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec,
-                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd);
+                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd, 0u,
+                                           clamp_span(a.p.span, a.limit, (uint64_t)obj * a.obj_stride));
 }
 
 // Mixed erasure patterns in one launch: each workgroup reads its object's
@@ -296,16 +326,17 @@ __global__ __launch_bounds__(BS) void gf_apply_multi(const MultiArgs<K, R> m) {
         const uint32_t obj = m.objs[item * m.opw + j];
         if (obj == 0xffffffffu) return;
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(m.base, obj, p, m.nvec, m.tail, m.bad, threadIdx.x - j * m.nvec,
-                                               Redirect(), obj * (uint32_t)m.obj_stride, m.gspan);
+                                               Redirect(), obj * (uint32_t)m.obj_stride, m.gspan);  // gspan <= limit
         return;
     }
     const uint32_t obj = ((constant_ptr<uint32_t>)m.objs)[item];
     const uint32_t pi = ((constant_ptr<uint32_t>)m.obj_pass)[item];
     const __attribute__((address_space(4))) Pass<K, R> &p = ((constant_ptr<Pass<K, R>>)m.passes)[pi];
     const uint8_t *ob = m.base + (uint64_t)obj * m.obj_stride;
+    const uint32_t span = clamp_span(p.span, m.limit, (uint64_t)obj * m.obj_stride);
     for (int ch = 0; ch < CH; ++ch)
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(ob, obj, p, m.nvec, m.tail, m.bad,
-                                               (chunk * CH + ch) * (BS * U) + threadIdx.x);
+                                               (chunk * CH + ch) * (BS * U) + threadIdx.x, Redirect(), 0u, span);
 }
 
 }  // namespace rsgpu

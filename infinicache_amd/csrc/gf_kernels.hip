@@ -95,6 +95,7 @@ struct GenericArgs {
     const uint32_t *tab;     // [K][rstride][kTabWords], pre-offset to this pass's first row
     const uint32_t *in_row;  // [K] row indices; offset = row * pitch
     uint32_t nvec, tail, nw, span, K, rstride, pitch, clear, packed;
+    uint64_t limit;  // bytes readable from base (ApplyArgs::limit)
     Order ord;  // item = object
     uint32_t out_off[kMaxRG];
 };
@@ -106,8 +107,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     const uint32_t v = chunk * kBlock + threadIdx.x;
     if (v >= a.nvec) return;
     const uint8_t *ob = a.base + (uint64_t)obj * a.obj_stride;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)ob, (short)0, (int)clamp_span(a.span, a.limit, (uint64_t)obj * a.obj_stride), 0x00020000);
     const uint32_t voff = v * 16u;
     const constant_ptr<uint32_t> tab = (constant_ptr<uint32_t>)a.tab;
     const constant_ptr<uint32_t> rows = (constant_ptr<uint32_t>)a.in_row;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     for (int r = 0; r < R; ++r) {
         if ((uint32_t)r < a.nw) {
             u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-            store_row<kStoreAux>(o, rs, voff, a.out_off[r], a.packed && v == a.nvec - 1, a.tail);
+            store_row<kStoreAux>(o, rs, voff, a.out_off[r], v == a.nvec - 1 ? a.packed : 0u);
         } else {
             const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
 #pragma unroll
@@ -164,6 +165,19 @@ struct Sub {  // one pass over <= kMaxR output rows of a plan
     int r0, R, nw;
 };
 
+// bytes an object's rows occupy for this plan (through its highest row)
+size_t rows_extent(const Plan &p, size_t pitch) {
+    int maxrow = 0;
+    for (int r : p.in_rows) maxrow = std::max(maxrow, r);
+    for (int r : p.out_rows) maxrow = std::max(maxrow, r);
+    return (size_t)(maxrow + 1) * pitch;
+}
+
+// ApplyArgs/MultiArgs/GenericArgs::limit for `no` objects from a launch base
+uint64_t launch_limit(const Plan &p, const Layout &L, size_t no) {
+    return (uint64_t)(no ? no - 1 : 0) * L.obj_stride + rows_extent(p, L.pitch);
+}
+
 template <int K, int R>
 void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool have_bad, Pass<K, R> &a) {
     a.nw = (uint32_t)s.nw;
@@ -171,7 +185,7 @@ void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool ha
     // pass is the plan's last pass (it holds those rows at the same offsets)
     a.ki = (s.r0 + R == p.R) ? (uint32_t)std::min(p.ki, R) : 0u;
     a.clear = (have_bad && p.nw == p.R) ? 1u : 0u;
-    a.packed = (pitch % 16) != 0;
+    a.packed = tail_part(pitch, nvec);
     int maxrow = 0;
     for (int c = 0; c < K; ++c) {
         a.in_off[c] = (uint32_t)(p.in_rows[c] * pitch);
@@ -217,6 +231,7 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
                 a.base = L.base + o0 * L.obj_stride;
                 a.bad = d_bad ? d_bad + o0 : nullptr;
                 a.nobj = (uint32_t)std::min<size_t>((size_t)ng * opw, (size_t)L.nobj - o0);
+                a.limit = launch_limit(p, L, a.nobj);
                 unsigned grid;
                 a.ord = make_order(1, (uint32_t)ng, (size_t)a.nobj * L.obj_stride, grid);
                 // (staging the group through LDS so that every wave load is
@@ -241,6 +256,7 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
         a.in_span = (uint32_t)std::min<size_t>(L.in_span, 0xffffffffu);
         a.copy_in = L.copy_in ? 1u : 0u;
         a.bad = d_bad ? d_bad + o0 : nullptr;
+        a.limit = launch_limit(p, L, (size_t)no);
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
         hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
@@ -301,7 +317,12 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
     uint32_t maxobj = 0;
     for (const Entry *e : es)
         for (uint32_t o : e->objs) maxobj = std::max(maxobj, o);
-    const size_t gspan = (size_t)maxobj * L.obj_stride + (size_t)L.pitch * 256;  // >= any pass span
+    // readable bytes from the batch base: through the highest row any of the
+    // class's plans uses in the batch's last object (see ApplyArgs::limit)
+    size_t ext = 0;
+    for (const Entry *e : es) ext = std::max(ext, rows_extent(*e->plan, L.pitch));
+    const uint64_t limit = (uint64_t)(L.nobj - 1) * L.obj_stride + ext;
+    const size_t gspan = std::min<uint64_t>((size_t)maxobj * L.obj_stride + (size_t)L.pitch * 256, limit);
     if (kUnroll == 1 && nvec * 2 <= kBlock && gspan <= 0xffffffffull) {
         const uint32_t opw = kBlock / nvec;
         size_t ngroups = 0;
@@ -330,6 +351,7 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
             m.obj_pass = m.objs + ngroups * opw;
             m.opw = opw;
             m.gspan = (uint32_t)gspan;
+            m.limit = limit;
             unsigned grid;
             m.ord = make_order(1, (uint32_t)ngroups, gspan, grid);
             hipLaunchKernelGGL((gf_apply_multi<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kMultiChunks>),
@@ -357,6 +379,7 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
         MultiArgs<K, R> m;
         m.opw = 1;
         m.gspan = 0;
+        m.limit = limit;
         m.base = L.base;
         m.obj_stride = L.obj_stride;
         m.bad = d_bad;
@@ -432,7 +455,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     a.tab = p.d_tab + (size_t)s.r0 * kTabWords;
     a.in_row = p.d_in_row;
     a.pitch = (uint32_t)L.pitch;
-    a.packed = (L.pitch % 16) != 0;
+    a.packed = tail_part(L.pitch, a.nvec);
     int maxrow = 0;
     for (int c = 0; c < K; ++c) maxrow = std::max(maxrow, p.in_rows[c]);
     for (int r = 0; r < R; ++r) {
@@ -448,6 +471,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.base = L.base + (size_t)o0 * L.obj_stride;
         a.bad = d_bad ? d_bad + o0 : nullptr;
         a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
+        a.limit = launch_limit(p, L, (size_t)no);
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
         // full occupancy: the wide generic passes are VALU-bound (tools/kbench

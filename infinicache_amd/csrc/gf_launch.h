@@ -64,6 +64,13 @@ inline Order make_order(uint32_t nchunk, uint32_t nitem, size_t span, unsigned &
 // items per launch so that the 1D grid stays below 2^31 workgroups
 inline int max_items(unsigned nchunk) { return (int)std::max(1u, 0x7ff00000u / std::max(1u, nchunk)); }
 
+// store_row's `part`: bytes of a row's last 16-B vector that may be written
+// when the next row starts within it (pitch < 16 * nvec), else 0
+inline uint32_t tail_part(size_t pitch, uint32_t nvec) {
+    const size_t w = pitch - (size_t)(nvec - 1) * 16;
+    return w < 16 ? (uint32_t)w : 0u;
+}
+
 // bytes covered by `no` objects of layout L (one object: its own span)
 inline size_t objs_span(const Layout &L, int no, size_t one) {
     return no > 1 ? (size_t)no * L.obj_stride : one;

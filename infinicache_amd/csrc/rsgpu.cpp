@@ -410,8 +410,10 @@ int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_
                  size_t obj_stride, int nobj) {
     if (!base || nobj < 0) return RSGPU_ERR_INVALID_ARG;
     if (shard_len == 0) return RSGPU_ERR_SHARD_NO_DATA;
-    if (((uintptr_t)base & 15) || (pitch & 15) || (obj_stride & 15)) return RSGPU_ERR_INVALID_ARG;
-    if (pitch < round_up(shard_len, 16)) return RSGPU_ERR_INVALID_ARG;
+    // any alignment: a pitch below 16 * ceil(S / 16) stores the last vector
+    // of a row in 8/4/2/1-byte pieces (store_row); 16-B aligned rows and
+    // objects are the fast path
+    if (pitch < shard_len) return RSGPU_ERR_INVALID_ARG;
     if ((size_t)ctx->n * pitch >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
     if (nobj > 1 && obj_stride < (size_t)ctx->n * pitch) return RSGPU_ERR_INVALID_ARG;
     return RSGPU_OK;
@@ -477,6 +479,7 @@ int dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shar
     if (!ctx || (nobj > 0 && !d_masks)) return RSGPU_ERR_INVALID_ARG;
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
+    if (((uintptr_t)d_base & 15) || (pitch & 15) || (obj_stride & 15)) return RSGPU_ERR_INVALID_ARG;
     if (ctx->n > kAtlasMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
@@ -1003,7 +1006,7 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     if (e) return e;
     const int n = ctx->n;
     if (nobj == 0) return RSGPU_OK;
-    if (n <= kAtlasMaxN)
+    if (n <= kAtlasMaxN && !((uintptr_t)d_base & 15) && !(pitch & 15) && !(obj_stride & 15))
         return recon_dev_multi_atlas(ctx, d_base, present, shard_len, pitch, obj_stride, nobj,
                                      check ? kAtlasDecode : data_only ? kAtlasData : kAtlasReconstruct, d_bad,
                                      stream);

@@ -444,16 +444,22 @@ def test_dev_many_objects_grid_y_split(gpu):
             assert np.array_equal(h[o, k + r], want[r]), o
 
 
-@pytest.mark.parametrize("k,p,S,nobj,gap", [(10, 2, 103, 1001, 0), (10, 2, 410, 257, 48), (10, 4, 1, 700, 0),
-                                            (10, 2, 17, 513, 16), (12, 4, 2048, 33, 0), (10, 2, 2049, 9, 0),
-                                            (3, 1, 1000, 100, 4096)])
-def test_dev_small_objects_packed_workgroups(gpu, k, p, S, nobj, gap):
+@pytest.mark.parametrize("k,p,S,nobj,gap,palign", [(10, 2, 103, 1001, 0, 16), (10, 2, 410, 257, 48, 16),
+                                                   (10, 4, 1, 700, 0, 16), (10, 2, 17, 513, 16, 16),
+                                                   (12, 4, 2048, 33, 0, 16), (10, 2, 2049, 9, 0, 16),
+                                                   (3, 1, 1000, 100, 4096, 16),
+                                                   (10, 2, 103, 1001, 0, 4), (10, 2, 103, 999, 0, 1),
+                                                   (10, 4, 1, 700, 0, 1), (10, 2, 17, 513, 3, 1),
+                                                   (10, 2, 4097, 20, 0, 1), (6, 3, 29, 300, 5, 4)])
+def test_dev_small_objects_packed_workgroups(gpu, k, p, S, nobj, gap, palign):
     """Rows of <= 128 vectors: a workgroup codes 256 // nvec whole objects
     (gf_kernels.hip launch_fixed, opw > 1).  Encode the whole batch against
     the oracle, per-object Verify flags, fused decode and data-only
-    reconstruct; ragged last group, strides with gaps between objects."""
+    reconstruct; ragged last group, strides with gaps between objects.
+    palign < 16: pitches below 16 * ceil(S / 16) down to byte-packed rows
+    (pitch = S) and unaligned object strides; nothing past S is written."""
     n = k + p
-    pitch = (S + 15) // 16 * 16
+    pitch = (S + palign - 1) // palign * palign
     stride = n * pitch + gap
     g = torch.Generator(device="cuda").manual_seed(S * 7 + nobj)
     flat = torch.randint(0, 256, (nobj * stride,), dtype=torch.uint8, device="cuda", generator=g)
@@ -691,3 +697,41 @@ def test_dev_single_100mib_object(gpu):
     assert int(bad.sum()) == 0
     assert torch.equal(b[0, :k], orig)
     assert np.array_equal(b[0, 10].cpu().numpy(), par[0])
+
+
+@pytest.mark.parametrize("palign", [4, 1])
+def test_dev_packed_rows_batch_ends_at_allocation_end(gpu, palign):
+    """Pitch below 16 * ceil(S / 16): a row's last 16-B vector reaches past its
+    pitch, and for the batch's last object past the caller's buffer.  The
+    launch clamps its buffer ranges so nothing is read there: here the batch
+    is sized to end exactly at the end of its 2 MiB-granular allocation
+    (1 KiB objects, S = 103, as the reference's example object)."""
+    k, p, S = 10, 2, 103
+    n = k + p
+    pitch = (S + palign - 1) // palign * palign
+    stride = n * pitch
+    # nobj * stride a whole number of 2 MiB blocks
+    import math
+    nobj = (2 << 20) // math.gcd(stride, 2 << 20)
+    flat = torch.randint(0, 256, (nobj * stride,), dtype=torch.uint8, device="cuda")
+    b = flat.view(nobj, n, pitch)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(flat, S, pitch, stride, nobj, s)
+    torch.cuda.synchronize()
+    h = b.cpu().numpy()
+    m = enc.matrix()
+    for o in (0, nobj // 2, nobj - 2, nobj - 1):
+        want = oracle.apply(m[k:], [h[o, c, :S] for c in range(k)])
+        for r in range(p):
+            assert np.array_equal(h[o, k + r, :S], want[r]), o
+    golden = b.clone()
+    b[:, 0, :S] = 0
+    b[:, 11, :S] = 0
+    present = [i not in (0, 11) for i in range(n)]
+    bad = torch.full((nobj,), 3, dtype=torch.int32, device="cuda")
+    enc.decode_dev(flat, present, S, pitch, stride, nobj, bad, s)
+    enc.verify_dev(flat, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert not bad.any()
+    assert torch.equal(b[:, :, :S], golden[:, :, :S])

@@ -5,7 +5,9 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-crashed() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+# any failing step ends the session: a Python exception may hide a GPU memory
+# fault (hipErrorIllegalAddress), after which nothing more may run on the GPU
+crashed() { [ "$1" != 0 ]; }
 run() {  # run <name> <timeout> cmd...
   local name=$1 t=$2; shift 2
   echo "== $name: $*" | tee -a gpurun_out/steps.log
@@ -13,7 +15,7 @@ run() {  # run <name> <timeout> cmd...
   local rc=$?
   echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
   tail -5 "gpurun_out/$name.log"
-  if crashed $rc; then echo "CRASH in $name; stopping"; exit $rc; fi
+  if crashed $rc; then echo "FAILED: $name (rc=$rc); stopping"; exit $rc; fi
   return 0
 }
 STEPS=${STEPS:-"pytest smoke bench prof"}
@@ -33,6 +35,13 @@ for s in $STEPS; do
     prof_mixed) for wl in small_mixed encdec_mixed; do
               run prof_$wl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 --workload $wl
             done ;;
+    small1k) for wl in ${SMALL_WLS:-small1k small1k_p4 small1k_p1}; do
+              run bench_$wl 300 python bench.py --workload $wl --no-cpu
+              run prof_$wl 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 10 --workload $wl
+              run pmc_fetch_$wl 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --workload $wl
+              run pmc_write_$wl 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --workload $wl
+            done ;;
+    avail)  run avail 120 rocprofv3 --list-avail ;;
     pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
     torchrun1) run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --no-cpu ;;
