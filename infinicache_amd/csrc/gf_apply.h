@@ -66,6 +66,11 @@ struct Layout {
     const uint8_t *in_base = nullptr;
     size_t in_span = 0;           // bytes readable from in_base
     bool copy_in = false;         // input rows copied into base as well
+    // at least 16 readable bytes follow the last object's rows (the library's
+    // own staging images).  Without it, a layout whose rows' last 16-B vector
+    // reaches past the pitch (pitch < 16 * ceil(S / 16)) codes its last object
+    // through a scratch copy, so no load runs past the caller's buffer.
+    bool slack = false;
 };
 constexpr int kRedirectMaxK = 16;  // passes that can redirect their written rows
 

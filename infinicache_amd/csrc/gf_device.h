@@ -137,21 +137,9 @@ struct ApplyArgs {  // one pass for every object of the launch (kernarg)
     uint32_t opw;    // objects per workgroup (> 1: small objects, item = group of opw)
     uint32_t nobj;   // objects in the launch (bounds the last group when opw > 1)
     uint32_t gspan;  // opw > 1: bytes a group's objects cover from the first one's base
-    // bytes readable from base: the rows of the launch's last object end here.
-    // A row's last 16-B vector may reach up to 15 bytes past its pitch; the
-    // ranges are clamped to this so the last object never reads past the
-    // caller's buffer (those bytes only feed pad bytes)
-    uint64_t limit;
     Order ord;       // item = object, or group of opw objects
     Pass<K, R> p;
 };
-
-// buffer-range bytes for an object (or group) at offset `at` from the launch
-// base: its span, clamped to the launch's readable limit
-__device__ __forceinline__ uint32_t clamp_span(uint32_t span, uint64_t limit, uint64_t at) {
-    const uint64_t left = limit > at ? limit - at : 0;
-    return left < span ? (uint32_t)left : span;
-}
 
 template <int K, int R>
 struct MultiArgs {  // per-object passes (a Get batch with mixed erasure patterns)
@@ -167,7 +155,6 @@ struct MultiArgs {  // per-object passes (a Get batch with mixed erasure pattern
     // pass, objs[i*opw + j] (~0u: empty slot), passes[obj_pass[i]]; lanes
     // address object o at o * obj_stride from base, within gspan bytes
     uint32_t opw, gspan;
-    uint64_t limit;  // bytes readable from base (see ApplyArgs::limit)
 };
 
 // One workgroup = BS lanes x U vectors of 16 B of one object (grid.y).
@@ -289,8 +276,7 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
         if (j >= a.opw || o0 + j >= a.nobj) return;
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)o0 * a.obj_stride, o0 + j, a.p, a.nvec,
                                                a.tail, a.bad, threadIdx.x - j * a.nvec, Redirect(),
-                                               j * (uint32_t)a.obj_stride,
-                                               clamp_span(a.gspan, a.limit, (uint64_t)o0 * a.obj_stride));
+                                               j * (uint32_t)a.obj_stride, a.gspan);
         return;
     }
     Redirect rd;
@@ -300,8 +286,7 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
     rd.out = a.out_base;
     rd.dual = a.out_dual != 0;
     gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec,
-                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd, 0u,
-                                           clamp_span(a.p.span, a.limit, (uint64_t)obj * a.obj_stride));
+                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd);
 }
 
 // Mixed erasure patterns in one launch: each workgroup reads its object's
@@ -326,17 +311,16 @@ __global__ __launch_bounds__(BS) void gf_apply_multi(const MultiArgs<K, R> m) {
         const uint32_t obj = m.objs[item * m.opw + j];
         if (obj == 0xffffffffu) return;
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(m.base, obj, p, m.nvec, m.tail, m.bad, threadIdx.x - j * m.nvec,
-                                               Redirect(), obj * (uint32_t)m.obj_stride, m.gspan);  // gspan <= limit
+                                               Redirect(), obj * (uint32_t)m.obj_stride, m.gspan);
         return;
     }
     const uint32_t obj = ((constant_ptr<uint32_t>)m.objs)[item];
     const uint32_t pi = ((constant_ptr<uint32_t>)m.obj_pass)[item];
     const __attribute__((address_space(4))) Pass<K, R> &p = ((constant_ptr<Pass<K, R>>)m.passes)[pi];
     const uint8_t *ob = m.base + (uint64_t)obj * m.obj_stride;
-    const uint32_t span = clamp_span(p.span, m.limit, (uint64_t)obj * m.obj_stride);
     for (int ch = 0; ch < CH; ++ch)
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(ob, obj, p, m.nvec, m.tail, m.bad,
-                                               (chunk * CH + ch) * (BS * U) + threadIdx.x, Redirect(), 0u, span);
+                                               (chunk * CH + ch) * (BS * U) + threadIdx.x);
 }
 
 }  // namespace rsgpu

@@ -95,7 +95,6 @@ struct GenericArgs {
     const uint32_t *tab;     // [K][rstride][kTabWords], pre-offset to this pass's first row
     const uint32_t *in_row;  // [K] row indices; offset = row * pitch
     uint32_t nvec, tail, nw, span, K, rstride, pitch, clear, packed;
-    uint64_t limit;  // bytes readable from base (ApplyArgs::limit)
     Order ord;  // item = object
     uint32_t out_off[kMaxRG];
 };
@@ -107,8 +106,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     const uint32_t v = chunk * kBlock + threadIdx.x;
     if (v >= a.nvec) return;
     const uint8_t *ob = a.base + (uint64_t)obj * a.obj_stride;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)ob, (short)0, (int)clamp_span(a.span, a.limit, (uint64_t)obj * a.obj_stride), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
     const uint32_t voff = v * 16u;
     const constant_ptr<uint32_t> tab = (constant_ptr<uint32_t>)a.tab;
     const constant_ptr<uint32_t> rows = (constant_ptr<uint32_t>)a.in_row;
@@ -173,10 +172,6 @@ size_t rows_extent(const Plan &p, size_t pitch) {
     return (size_t)(maxrow + 1) * pitch;
 }
 
-// ApplyArgs/MultiArgs/GenericArgs::limit for `no` objects from a launch base
-uint64_t launch_limit(const Plan &p, const Layout &L, size_t no) {
-    return (uint64_t)(no ? no - 1 : 0) * L.obj_stride + rows_extent(p, L.pitch);
-}
 
 template <int K, int R>
 void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool have_bad, Pass<K, R> &a) {
@@ -231,7 +226,6 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
                 a.base = L.base + o0 * L.obj_stride;
                 a.bad = d_bad ? d_bad + o0 : nullptr;
                 a.nobj = (uint32_t)std::min<size_t>((size_t)ng * opw, (size_t)L.nobj - o0);
-                a.limit = launch_limit(p, L, a.nobj);
                 unsigned grid;
                 a.ord = make_order(1, (uint32_t)ng, (size_t)a.nobj * L.obj_stride, grid);
                 // (staging the group through LDS so that every wave load is
@@ -256,7 +250,6 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
         a.in_span = (uint32_t)std::min<size_t>(L.in_span, 0xffffffffu);
         a.copy_in = L.copy_in ? 1u : 0u;
         a.bad = d_bad ? d_bad + o0 : nullptr;
-        a.limit = launch_limit(p, L, (size_t)no);
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
         hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
@@ -317,12 +310,7 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
     uint32_t maxobj = 0;
     for (const Entry *e : es)
         for (uint32_t o : e->objs) maxobj = std::max(maxobj, o);
-    // readable bytes from the batch base: through the highest row any of the
-    // class's plans uses in the batch's last object (see ApplyArgs::limit)
-    size_t ext = 0;
-    for (const Entry *e : es) ext = std::max(ext, rows_extent(*e->plan, L.pitch));
-    const uint64_t limit = (uint64_t)(L.nobj - 1) * L.obj_stride + ext;
-    const size_t gspan = std::min<uint64_t>((size_t)maxobj * L.obj_stride + (size_t)L.pitch * 256, limit);
+    const size_t gspan = (size_t)maxobj * L.obj_stride + (size_t)L.pitch * 256;  // >= any pass span
     if (kUnroll == 1 && nvec * 2 <= kBlock && gspan <= 0xffffffffull) {
         const uint32_t opw = kBlock / nvec;
         size_t ngroups = 0;
@@ -351,7 +339,6 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
             m.obj_pass = m.objs + ngroups * opw;
             m.opw = opw;
             m.gspan = (uint32_t)gspan;
-            m.limit = limit;
             unsigned grid;
             m.ord = make_order(1, (uint32_t)ngroups, gspan, grid);
             hipLaunchKernelGGL((gf_apply_multi<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kMultiChunks>),
@@ -379,7 +366,6 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
         MultiArgs<K, R> m;
         m.opw = 1;
         m.gspan = 0;
-        m.limit = limit;
         m.base = L.base;
         m.obj_stride = L.obj_stride;
         m.bad = d_bad;
@@ -471,7 +457,6 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.base = L.base + (size_t)o0 * L.obj_stride;
         a.bad = d_bad ? d_bad + o0 : nullptr;
         a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
-        a.limit = launch_limit(p, L, (size_t)no);
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
         // full occupancy: the wide generic passes are VALU-bound (tools/kbench
@@ -506,7 +491,54 @@ fixed_fn pick_fixed(int K, int R) {
 
 }  // namespace
 
+namespace {
+
+// the rows' last 16-B vector reaches past the pitch, and nothing guarantees
+// readable bytes after the last object (Layout::slack)
+bool overhangs(const Layout &L) {
+    return !L.slack && !L.in_base && !L.out_base && (L.shard_len + 15) / 16 * 16 > L.pitch;
+}
+
+hipError_t launch_plan_core(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st);
+
+// The batch's last object of an overhanging layout, coded in a stream-ordered
+// scratch copy with slack: copy its rows in, run the pass, copy the written
+// rows back (every byte of a written row up to its pitch is the pass's).
+hipError_t launch_last_object(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
+    uint8_t *obj = L.base + (size_t)(L.nobj - 1) * L.obj_stride;
+    const size_t ext = rows_extent(p, L.pitch);
+    uint8_t *tmp = nullptr;
+    hipError_t e = hipMallocAsync((void **)&tmp, ext + 64, st);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(tmp, obj, ext, hipMemcpyDeviceToDevice, st);
+    Layout one{tmp, L.obj_stride, L.pitch, L.shard_len, 1};
+    one.slack = true;
+    if (e == hipSuccess) e = launch_plan_core(p, one, d_bad ? d_bad + (L.nobj - 1) : nullptr, st);
+    for (int r = 0; r < p.nw && e == hipSuccess; ++r)
+        e = hipMemcpyAsync(obj + (size_t)p.out_rows[r] * L.pitch, tmp + (size_t)p.out_rows[r] * L.pitch, L.pitch,
+                           hipMemcpyDeviceToDevice, st);
+    const hipError_t f = hipFreeAsync(tmp, st);
+    return e != hipSuccess ? e : f;
+}
+
+}  // namespace
+
 hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
+    if (L.nobj <= 0 || p.R <= 0) return hipSuccess;
+    if (overhangs(L)) {
+        // every object's over-read lands in the next object, except the last one's
+        Layout head = L;
+        head.nobj = L.nobj - 1;
+        head.slack = true;
+        hipError_t e = launch_plan_core(p, head, d_bad, st);
+        return e != hipSuccess ? e : launch_last_object(p, L, d_bad, st);
+    }
+    return launch_plan_core(p, L, d_bad, st);
+}
+
+namespace {
+
+hipError_t launch_plan_core(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
     if (L.nobj <= 0 || p.R <= 0) return hipSuccess;
     static_assert(kRedirectMaxK == kMaxK, "redirect limit");
     if ((L.out_base || L.in_base) && (p.K > kMaxK || L.nobj != 1))
@@ -541,6 +573,8 @@ hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
     return hipSuccess;
 }
 
+}  // namespace
+
 MultiWorkspace::~MultiWorkspace() {
     for (auto &u : uploaded)
         if (u) (void)hipEventDestroy(u);
@@ -552,8 +586,27 @@ MultiWorkspace::~MultiWorkspace() {
     }
 }
 
+hipError_t launch_plans_multi_core(const std::vector<Plan *> &plans, const std::vector<int> &plan_of,
+                                   const Layout &L, uint32_t *d_bad, hipStream_t st, MultiWorkspace &ws);
+
 hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vector<int> &plan_of,
                               const Layout &L, uint32_t *d_bad, hipStream_t st, MultiWorkspace &ws) {
+    if (L.nobj > 0 && overhangs(L)) {  // the last object through launch_plan's scratch copy
+        Layout head = L;
+        head.nobj = L.nobj - 1;
+        head.slack = true;
+        std::vector<int> po(plan_of.begin(), plan_of.begin() + head.nobj);
+        hipError_t e = launch_plans_multi_core(plans, po, head, d_bad, st, ws);
+        const int last = plan_of[L.nobj - 1];
+        if (e != hipSuccess || last < 0) return e;
+        Layout one{L.base + (size_t)(L.nobj - 1) * L.obj_stride, L.obj_stride, L.pitch, L.shard_len, 1};
+        return launch_plan(*plans[last], one, d_bad ? d_bad + (L.nobj - 1) : nullptr, st);
+    }
+    return launch_plans_multi_core(plans, plan_of, L, d_bad, st, ws);
+}
+
+hipError_t launch_plans_multi_core(const std::vector<Plan *> &plans, const std::vector<int> &plan_of,
+                                   const Layout &L, uint32_t *d_bad, hipStream_t st, MultiWorkspace &ws) {
     // entries grouped into (K, R) classes; K > 16 plans run object by object
     std::vector<std::vector<Entry>> per_plan(plans.size());
     std::vector<std::vector<uint32_t>> objs_of(plans.size());
@@ -568,6 +621,7 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
         if (p.K > kMaxK) {
             for (uint32_t o : objs_of[i]) {
                 Layout one{L.base + (size_t)o * L.obj_stride, L.obj_stride, L.pitch, L.shard_len, 1};
+                one.slack = L.slack || (int)o + 1 < L.nobj;  // the next object follows
                 hipError_t e = launch_plan(p, one, d_bad ? d_bad + o : nullptr, st);
                 if (e != hipSuccess) return e;
             }

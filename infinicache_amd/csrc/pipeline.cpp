@@ -69,6 +69,13 @@ int ensure_flags(rsgpu_ctx *ctx, int nobj) {
     return RSGPU_OK;
 }
 
+// one object in a pipeline slot (capacity >= n*S + 16: readable slack)
+Layout slack_layout(uint8_t *d, size_t pitch, size_t S) {
+    Layout L{d, 0, pitch, S, 1};
+    L.slack = true;
+    return L;
+}
+
 int drain(rsgpu_ctx *ctx) {
     hipError_t first = hipSuccess;
     for (auto &s : ctx->pipe.slots) {
@@ -222,7 +229,9 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
         PipeSlot &s = *ctx->pipe.slots[o % kSlots];
         const size_t S = shard_lens[o];
         he = hipMemcpyAsync(s.d, objs[o], (size_t)k * S, hipMemcpyHostToDevice, s.stream);
-        if (he == hipSuccess) he = launch_plan(*plan, Layout{s.d, 0, S, S, 1}, nullptr, s.stream);
+        Layout L{s.d, 0, S, S, 1};
+        L.slack = true;  // slot capacity >= n*S + 16
+        if (he == hipSuccess) he = launch_plan(*plan, L, nullptr, s.stream);
         if (he == hipSuccess)
             he = hipMemcpyAsync(objs[o] + (size_t)k * S, s.d + (size_t)k * S, (size_t)p * S,
                                 hipMemcpyDeviceToHost, s.stream);
@@ -297,7 +306,7 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
                                 hipMemcpyHostToDevice, s.stream);
         if (he == hipSuccess && checks) he = hipMemsetAsync(s.d_bad, 0, 4, s.stream);
         if (he == hipSuccess)
-            he = launch_plan(plan, Layout{s.d, 0, P, S, 1}, checks ? s.d_bad : nullptr, s.stream);
+            he = launch_plan(plan, slack_layout(s.d, P, S), checks ? s.d_bad : nullptr, s.stream);
         for (int r = 0; r < plan.nw && he == hipSuccess; ++r)
             he = hipMemcpyAsync(row[plan.out_rows[r]], s.d + (size_t)plan.out_rows[r] * P, S,
                                 hipMemcpyDeviceToHost, s.stream);

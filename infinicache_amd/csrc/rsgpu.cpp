@@ -194,6 +194,7 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     // following plan (`then`) reads the image, so the pass copies the input
     // rows into it as well.
     Layout L{s->d, 0, size, size, 1};
+    L.slack = true;  // the slot holds nrows_staged*size + 16 bytes at least
     if (split && plan.K <= kRedirectMaxK) {
         const size_t first = (size_t)rlo * size, need = (size_t)rhi * size + round_up(size, 16);
         if (const uint8_t *d = (const uint8_t *)host_device_ptr(span0, need - first)) {
@@ -273,7 +274,9 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         // on a side stream to overlap this kernel was measured slower: 67.5 ->
         // 85.7 us per fused encode+verify; the cross-stream event and second
         // sync cost more than the overlap.)
-        he = launch_plan(*then, Layout{s->d, 0, size, size, 1}, s->m_bad, s->stream);
+        Layout img{s->d, 0, size, size, 1};
+        img.slack = true;
+        he = launch_plan(*then, img, s->m_bad, s->stream);
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
     if (he != hipSuccess) {
