@@ -51,6 +51,9 @@ for s in $STEPS; do
               run kbench_$sh 300 ./tools/kbench $sh 15
             done ;;
     lat)    run lat_bench 300 ./tools/lat_bench 300 2 ;;
+    kgen)   for sh in ${KGEN:-enc20_4 dec20_4 enc20_8 enc32_8 dec32_8 enc64_16}; do
+              run kgen_$sh 300 ./tools/kbench lib:$sh 15
+            done ;;
     cpuinfo) (nproc; grep -m1 "model name" /proc/cpuinfo; grep -o -w -e avx512bw -e avx2 -e gfni /proc/cpuinfo | sort | uniq -c; cat /sys/fs/cgroup/cpu.max) > gpurun_out/cpuinfo.log 2>&1 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 ;;
     pmc_all) for wl in enc dec4; do

@@ -1241,7 +1241,8 @@ int lib_time(std::string spec, int rounds) {
     const int n = k + p;
     rsgpu_ctx *ctx;
     if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
-    if (ctx->use_device()) { std::printf("no device\n"); return 1; }
+    DeviceGuard dg_;
+    if (ctx->use_device(dg_)) { std::printf("no device\n"); return 1; }
     std::shared_ptr<Plan> plan;
     std::vector<uint8_t> present(n, 1);
     if (op == "enc") plan = ctx->plan_encode();
@@ -1335,7 +1336,8 @@ int main(int argc, char **argv) {
     const size_t S = (nbytes + k - 1) / k;
     rsgpu_ctx *ctx;
     if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
-    if (ctx->use_device()) { std::printf("no device\n"); return 1; }
+    DeviceGuard dg_;
+    if (ctx->use_device(dg_)) { std::printf("no device\n"); return 1; }
     std::vector<uint8_t> present(n, 1);
     std::shared_ptr<Plan> plan;
     if (shape.rfind("enc", 0) == 0) {
