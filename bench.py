@@ -56,6 +56,21 @@ WORKLOADS = {
     "small1k_p1": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
                        palign=1, desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, "
                                       "byte-packed rows (pitch 103)"),
+    # shard-major batches ([shard][object]: shard i of all objects back to
+    # back, as InfiniCache ships shard i to Lambda node i): the batch is coded
+    # as one object per shard row, whatever the object size
+    "small1k_sm": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
+                       shard_major=True, oalign=1,
+                       desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, shard-major "
+                            "(pieces back to back, S = 103)"),
+    "small1k_sm_mixed": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
+                             shard_major=True, oalign=16, mixed=True,
+                             desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, shard-major "
+                                  "(16-B aligned pieces), per-object random erasure pair (device-resident "
+                                  "present masks)"),
+    "small_sm": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
+                     shard_major=True, oalign=1,
+                     desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, shard-major"),
     "small_mixed": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
                         palign=16, mixed=True,
                         desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, per-object "
@@ -84,6 +99,10 @@ METRICS = {
     "small": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
     "small_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 4 KiB objects",
     "small1k": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
+    "small1k_sm": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch), 1 KiB objects",
+    "small1k_sm_mixed": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch, mixed erasure "
+                        "patterns), 1 KiB objects",
+    "small_sm": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch), 4 KiB objects",
     "small1k_p4": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
     "small1k_p1": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
     "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
@@ -520,9 +539,14 @@ def main():
     if args.strong:
         nobj = shard_objects(nobj, rank, world)[1]
     S = (w["nbytes"] + k - 1) // k
-    pal = w.get("palign", 256)
-    pitch = (S + pal - 1) // pal * pal
-    stride = n * pitch
+    if w.get("shard_major"):  # [shard][object]: object o's piece of shard i at i*pitch + o*stride
+        oal = w.get("oalign", 1)
+        stride = (S + oal - 1) // oal * oal
+        pitch = (nobj * stride + 255) // 256 * 256
+    else:                     # [object][shard][pitch]
+        pal = w.get("palign", 256)
+        pitch = (S + pal - 1) // pal * pal
+        stride = n * pitch
     enc = ia.New(k, p, device=local)
     stream = torch.cuda.current_stream(dev)
 
@@ -535,8 +559,14 @@ def main():
     # warm rate is reported beside it as `warm_repeat`, never as `value`.
     copies = max(1, args.copies)
     g = torch.Generator(device=dev).manual_seed(0x1F1C + rank)
-    allbuf = torch.randint(0, 256, (copies, nobj, n, pitch), dtype=torch.uint8, device=dev, generator=g)
-    allbuf[..., S:] = 0
+    if w.get("shard_major"):
+        allbuf = torch.randint(0, 256, (copies, n, pitch), dtype=torch.uint8, device=dev, generator=g)
+        allbuf[..., nobj * stride:] = 0
+        if stride > S:  # zero pads between the pieces
+            allbuf[..., :nobj * stride].view(copies, n, nobj, stride)[..., S:] = 0
+    else:
+        allbuf = torch.randint(0, 256, (copies, nobj, n, pitch), dtype=torch.uint8, device=dev, generator=g)
+        allbuf[..., S:] = 0
     bufs = [allbuf[j] for j in range(copies)]
     bad = torch.zeros(nobj, dtype=torch.int32, device=dev)
     present = [i not in w["lost"] and i not in w.get("absent", ()) for i in range(n)]
@@ -686,7 +716,7 @@ def main():
         }
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not w.get("shard_major"):
         from oracle import rs_numpy as rn
         ns = min(256, nobj)  # 256 x 1.26 MB: well beyond the host's last-level cache
         gpu_sample = bufs[0][:ns].cpu().numpy()  # final GPU state of the sampled objects
@@ -722,6 +752,8 @@ def main():
                 "object_bytes": w["nbytes"],
                 "shard_len": S,
                 "pitch": pitch,
+                "obj_stride": stride,
+                "layout": "shard-major" if w.get("shard_major") else "object-major",
                 "batch_per_gpu": nobj,
                 "batch_copies": copies,
                 "decode_erasures": list(w["lost"]),

@@ -71,6 +71,8 @@ struct Layout {
     // reaches past the pitch (pitch < 16 * ceil(S / 16)) codes its last object
     // through a scratch copy, so no load runs past the caller's buffer.
     bool slack = false;
+    // shard-major batch seen as one object (launch_plan): Pass::sub_*
+    uint32_t sub_stride = 0, sub_len = 0, sub_n = 0;
 };
 constexpr int kRedirectMaxK = 16;  // passes that can redirect their written rows
 

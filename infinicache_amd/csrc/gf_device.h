@@ -95,6 +95,10 @@ struct Pass {
     uint32_t clear;  // the plan has no check rows: this pass zeroes bad[obj]
     uint32_t span;   // bytes addressable from an object base
     uint32_t packed; // bytes of a row's last vector that may be written when < 16, else 0 (store_row)
+    // shard-major batch coded as one object (launch_plan): the row holds
+    // sub_n objects' shards of sub_len bytes every sub_stride bytes; check
+    // flags and clears are per object, attributed by byte position
+    uint32_t sub_stride, sub_len, sub_n;
     uint32_t in_off[K];
     uint32_t out_off[R];
     uint32_t tab[K * R * kTabWords];  // input-major [K][R][kTabWords]: scalar loads per input
@@ -255,7 +259,19 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
             } else {
                 const uint32_t valid = (v == nvec - 1) ? tail : 16u;
 #pragma unroll
-                for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+                for (int d = 0; d < 4; ++d) {
+                    uint32_t m = acc[r][d] & tail_mask(d, valid);
+                    if (a.sub_stride) {  // shard-major: flag the object each nonzero byte belongs to
+                        while (m) {
+                            const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3, x = v * 16u + d * 4u + b;
+                            const uint32_t o = x / a.sub_stride;
+                            if (x - o * a.sub_stride < a.sub_len) bad[o] = 1u;  // gap bytes are pads
+                            m &= ~(0xffu << (8 * b));
+                        }
+                    } else {
+                        mismatch |= m != 0;
+                    }
+                }
             }
         }
     }
@@ -263,8 +279,17 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
     // live in mapped host memory); zeroing happens before the launch
     if (mismatch) bad[obj] = 1u;
     // the plan has no check rows: the pass itself clears the object's flag
-    // (saves the caller's memset launch on the decode hot path)
-    if (a.clear && v0 == 0) bad[obj] = 0u;
+    // (saves the caller's memset launch on the decode hot path); shard-major:
+    // the flags of the objects whose first byte is in this lane's vector
+    if (a.clear) {
+        if (a.sub_stride) {
+            const uint32_t x0 = v0 * 16u;
+            for (uint32_t o = (x0 + a.sub_stride - 1) / a.sub_stride; o < a.sub_n && o * a.sub_stride < x0 + 16u; ++o)
+                bad[o] = 0u;
+        } else if (v0 == 0) {
+            bad[obj] = 0u;
+        }
+    }
 }
 
 template <int K, int R, int U, int BS, int LAUX, int SAUX>

@@ -181,6 +181,7 @@ void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool ha
     a.ki = (s.r0 + R == p.R) ? (uint32_t)std::min(p.ki, R) : 0u;
     a.clear = (have_bad && p.nw == p.R) ? 1u : 0u;
     a.packed = tail_part(pitch, nvec);
+    a.sub_stride = a.sub_len = a.sub_n = 0;
     int maxrow = 0;
     for (int c = 0; c < K; ++c) {
         a.in_off[c] = (uint32_t)(p.in_rows[c] * pitch);
@@ -205,6 +206,9 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
     a.nvec = (uint32_t)((L.shard_len + 15) / 16);
     a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
     fill_pass<K, R>(p, s, L.pitch, a.nvec, d_bad != nullptr, a.p);
+    a.p.sub_stride = L.sub_stride;
+    a.p.sub_len = L.sub_len;
+    a.p.sub_n = L.sub_n;
     const unsigned gx = (a.nvec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
     // Small objects (a row of at most half a workgroup's vectors): one
     // workgroup codes opw whole objects, so its lanes stay busy (1 KiB
@@ -493,29 +497,37 @@ fixed_fn pick_fixed(int K, int R) {
 
 namespace {
 
-// the rows' last 16-B vector reaches past the pitch, and nothing guarantees
-// readable bytes after the last object (Layout::slack)
+// The batch's last object may read past the caller's buffer: a row's last
+// 16-B vector reaches past the row, and nothing guarantees readable bytes
+// after the batch (Layout::slack).  The caller's buffer spans every row's
+// full pitch.  Object-major ([object][shard]): the last row of the last
+// object ends at its pitch.  Shard-major ([shard][object], pitch >=
+// (nobj-1)*obj_stride + S): the last object's piece of the last shard row
+// ends where that row's pitch ends.
 bool overhangs(const Layout &L) {
-    return !L.slack && !L.in_base && !L.out_base && (L.shard_len + 15) / 16 * 16 > L.pitch;
+    if (L.slack || L.in_base || L.out_base) return false;
+    const size_t vec_end = (L.shard_len + 15) / 16 * 16;
+    const bool shard_major = L.nobj > 1 && L.pitch >= (size_t)(L.nobj - 1) * L.obj_stride + L.shard_len;
+    return (shard_major ? (size_t)(L.nobj - 1) * L.obj_stride : 0) + vec_end > L.pitch;
 }
 
 hipError_t launch_plan_core(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st);
 
 // The batch's last object of an overhanging layout, coded in a stream-ordered
-// scratch copy with slack: copy its rows in, run the pass, copy the written
-// rows back (every byte of a written row up to its pitch is the pass's).
+// scratch copy with slack: its rows copied in at a 16-B pitch (2D copy), the
+// pass run there, the written rows' shard_len bytes copied back.
 hipError_t launch_last_object(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
     uint8_t *obj = L.base + (size_t)(L.nobj - 1) * L.obj_stride;
-    const size_t ext = rows_extent(p, L.pitch);
+    const size_t P = (L.shard_len + 15) / 16 * 16, rows = rows_extent(p, 1);
     uint8_t *tmp = nullptr;
-    hipError_t e = hipMallocAsync((void **)&tmp, ext + 64, st);
+    hipError_t e = hipMallocAsync((void **)&tmp, rows * P + 64, st);
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(tmp, obj, ext, hipMemcpyDeviceToDevice, st);
-    Layout one{tmp, L.obj_stride, L.pitch, L.shard_len, 1};
+    e = hipMemcpy2DAsync(tmp, P, obj, L.pitch, L.shard_len, rows, hipMemcpyDeviceToDevice, st);
+    Layout one{tmp, 0, P, L.shard_len, 1};
     one.slack = true;
     if (e == hipSuccess) e = launch_plan_core(p, one, d_bad ? d_bad + (L.nobj - 1) : nullptr, st);
     for (int r = 0; r < p.nw && e == hipSuccess; ++r)
-        e = hipMemcpyAsync(obj + (size_t)p.out_rows[r] * L.pitch, tmp + (size_t)p.out_rows[r] * L.pitch, L.pitch,
+        e = hipMemcpyAsync(obj + (size_t)p.out_rows[r] * L.pitch, tmp + (size_t)p.out_rows[r] * P, L.shard_len,
                            hipMemcpyDeviceToDevice, st);
     const hipError_t f = hipFreeAsync(tmp, st);
     return e != hipSuccess ? e : f;
@@ -525,6 +537,25 @@ hipError_t launch_last_object(Plan &p, const Layout &L, uint32_t *d_bad, hipStre
 
 hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
     if (L.nobj <= 0 || p.R <= 0) return hipSuccess;
+    // Shard-major batch ([shard][object]: shard i of object o at
+    // base + i*pitch + o*obj_stride, the objects' pieces of one shard back to
+    // back): coding is byte-position-wise, so the batch IS one object whose
+    // shard is the whole row, streamed at the large-object rate however small
+    // the objects are.  Gaps between pieces (obj_stride up to roundup16(S))
+    // are pad bytes.  Check flags stay per object (Pass::sub_*); the generic
+    // kernel (K > 16) has no per-object attribution, so it converts only
+    // without flags.
+    const size_t row = (size_t)(L.nobj - 1) * L.obj_stride + L.shard_len;
+    if (L.nobj > 1 && !L.in_base && !L.out_base && L.sub_stride == 0 && L.obj_stride >= L.shard_len &&
+        L.obj_stride <= (L.shard_len + 15) / 16 * 16 && (row + 15) / 16 * 16 <= L.pitch &&
+        (p.K <= kMaxK || !d_bad) && (size_t)L.nobj * L.obj_stride < ((size_t)1 << 32)) {
+        Layout big{L.base, 0, L.pitch, row, 1};
+        big.slack = L.slack;
+        big.sub_stride = (uint32_t)L.obj_stride;
+        big.sub_len = (uint32_t)L.shard_len;
+        big.sub_n = (uint32_t)L.nobj;
+        return launch_plan(p, big, d_bad, st);
+    }
     if (overhangs(L)) {
         // every object's over-read lands in the next object, except the last one's
         Layout head = L;

@@ -418,7 +418,12 @@ int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_
     // objects are the fast path
     if (pitch < shard_len) return RSGPU_ERR_INVALID_ARG;
     if ((size_t)ctx->n * pitch >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
-    if (nobj > 1 && obj_stride < (size_t)ctx->n * pitch) return RSGPU_ERR_INVALID_ARG;
+    // objects must not overlap: object-major ([object][shard]: each object's
+    // rows within its stride) or shard-major ([shard][object]: each shard row
+    // holds every object's piece)
+    if (nobj > 1 && obj_stride < (size_t)ctx->n * pitch &&
+        !(obj_stride >= shard_len && pitch >= (size_t)(nobj - 1) * obj_stride + shard_len))
+        return RSGPU_ERR_INVALID_ARG;
     return RSGPU_OK;
 }
 

@@ -1,0 +1,136 @@
+"""Shard-major batches ([shard][object]: shard i of object o at
+base + i*pitch + o*obj_stride) against the CPU oracle, bit-exact.
+
+InfiniCache sends shard i of an object to Lambda node i (client/ecRedis.go
+EcSet, one RESP set per shard, :58-129); a batch laid out shard-major keeps
+each node's shards of many objects contiguous.  Coding is byte-position-wise,
+so such a batch is coded as ONE object whose shard is the whole row
+(gf_kernels.hip launch_plan): small objects stream at the large-object rate.
+Covered: pieces back to back (obj_stride = S) and 16-B aligned (gaps are pad
+bytes), per-object Verify flags and decode clears attributed by byte
+position, corrupted pad gaps not flagged, a tight pitch (the last object goes
+through the scratch path), K > 16, and the device-resolved mixed patterns."""
+import numpy as np
+import pytest
+
+import infinicache_amd as ia
+import oracle
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _batch(k, p, S, nobj, stride, pitch, seed):
+    n = k + p
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    flat = torch.zeros(n * pitch, dtype=torch.uint8, device="cuda")
+    rows = flat.view(n, pitch)
+    for i in range(n):  # only the pieces hold data; gaps and row tails zero
+        piece = torch.randint(0, 256, (nobj, S), dtype=torch.uint8, device="cuda", generator=g)
+        rows[i, :nobj * stride].view(nobj, stride)[:, :S] = piece if stride > S else piece
+    return flat, rows
+
+
+def _pieces(rows, i, nobj, S, stride):
+    return rows[i, :nobj * stride].view(nobj, stride)[:, :S]
+
+
+def _expect_parity(enc, rows, k, p, nobj, S, stride):
+    h = rows.cpu().numpy()
+    m = enc.matrix()
+    data = [h[i, :nobj * stride].reshape(nobj, stride)[:, :S].reshape(-1) for i in range(k)]
+    return oracle.apply(m[k:], data)  # the batch IS one object: one long row per shard
+
+
+@pytest.mark.parametrize("k,p,S,nobj,aligned", [(10, 2, 103, 5000, False), (10, 2, 103, 5000, True),
+                                                (10, 4, 1, 3000, False), (10, 2, 17, 777, True),
+                                                (10, 2, 4096, 300, False), (6, 3, 1000, 50, True),
+                                                (20, 4, 103, 600, False)])
+def test_shard_major_encode_verify_decode(gpu, k, p, S, nobj, aligned):
+    n = k + p
+    stride = (S + 15) // 16 * 16 if aligned else S
+    pitch = (nobj * stride + 255) // 256 * 256
+    flat, rows = _batch(k, p, S, nobj, stride, pitch, seed=S * 31 + nobj)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    before = rows.clone()
+    enc.encode_dev(flat, S, pitch, stride, nobj, s)
+    torch.cuda.synchronize()
+    want = _expect_parity(enc, before, k, p, nobj, S, stride)
+    for r in range(p):
+        got = _pieces(rows, k + r, nobj, S, stride).cpu().numpy().reshape(-1)
+        assert np.array_equal(got, want[r]), r
+    # data rows untouched
+    assert torch.equal(rows[:k], before[:k])
+    # Verify: per-object flags; garbage in the pad gaps is not a mismatch
+    hit = sorted({0, nobj - 1, nobj // 3})
+    for o in hit:
+        _pieces(rows, (o * 5) % n, nobj, S, stride)[o, (o * 7) % S] ^= 0x5A
+    if aligned and stride > S:
+        rows[:, :nobj * stride].view(n, nobj, stride)[:, 1::2, S:] = 0xEE  # pads
+    bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    enc.verify_dev(flat, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    if k <= 16:  # K <= 16: one launch over the whole row, flags by byte position
+        assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit
+    else:  # K > 16 with flags: per-object launches, same flags
+        assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit
+    for o in hit:
+        _pieces(rows, (o * 5) % n, nobj, S, stride)[o, (o * 7) % S] ^= 0x5A
+    golden = [_pieces(rows, i, nobj, S, stride).clone() for i in range(n)]
+    # fused decode (healthy Get: data 0 and k//2 lost) clears every flag
+    lost = (0, k // 2)
+    for i in lost:
+        _pieces(rows, i, nobj, S, stride).fill_(0xC3)
+    bad.fill_(7)
+    enc.decode_dev(flat, [i not in lost for i in range(n)], S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert not bad.any()
+    for i in range(n):
+        assert torch.equal(_pieces(rows, i, nobj, S, stride), golden[i]), i
+
+
+def test_shard_major_tight_pitch_last_object(gpu):
+    """pitch = (nobj-1)*stride + S exactly: the last object's piece ends the
+    row, its last 16-B vector would read past the batch; it is coded through
+    the scratch copy (and the conversion to one object is not taken)."""
+    k, p, S, nobj = 10, 2, 103, 1001
+    n = k + p
+    stride = S
+    pitch = (nobj - 1) * stride + S
+    flat = torch.randint(0, 256, (n * pitch,), dtype=torch.uint8, device="cuda")
+    rows = flat.view(n, pitch)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    before = rows.clone()
+    enc.encode_dev(flat, S, pitch, stride, nobj, s)
+    torch.cuda.synchronize()
+    want = _expect_parity(enc, before, k, p, nobj, S, stride)
+    for r in range(p):
+        assert np.array_equal(rows[k + r].cpu().numpy(), want[r]), r
+
+
+def test_shard_major_mixed_patterns_masks(gpu):
+    """Device-resolved mixed patterns on a shard-major batch (16-B aligned
+    pieces, as the masks calls require)."""
+    k, p, S, nobj = 10, 2, 103, 4000
+    n = k + p
+    stride = 112
+    pitch = nobj * stride
+    flat, rows = _batch(k, p, S, nobj, stride, pitch, seed=5)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(flat, S, pitch, stride, nobj, s)
+    golden = rows.clone()
+    rng = np.random.default_rng(3)
+    present = np.ones((nobj, n), dtype=np.uint8)
+    np.put_along_axis(present, np.argsort(rng.random((nobj, n)), axis=1)[:, :p], 0, axis=1)
+    view = rows.view(n, nobj, stride)
+    pm = torch.from_numpy(present.T.copy()).to("cuda").bool()
+    view[..., :S][~pm] = 0x77
+    masks = (present.astype(np.int64) << np.arange(n)).sum(axis=1).astype(np.int32)
+    status = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    enc.decode_dev_masks(flat, torch.from_numpy(masks).to("cuda"), S, pitch, stride, nobj, status, s)
+    torch.cuda.synchronize()
+    assert not status.any()
+    assert torch.equal(view[..., :S], golden.view(n, nobj, stride)[..., :S])
