@@ -44,6 +44,8 @@ for s in $STEPS; do
     avail)  run avail 120 rocprofv3 --list-avail ;;
     pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
+    rehearse2) BENCH_DIST_BACKEND=gloo BENCH_SHARE_GPU=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --no-cpu --copies 2 ;;
+    trace_dev) run bench_trace_dev 900 python bench.py --workload trace --steps 3 --warmup 1 --devices ${TRACE_DEVICES:-1} ;;
     torchrun1) run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --no-cpu ;;
     latency) run bench_latency 600 python bench.py --workload latency --steps 200 --warmup 10 ;;
     trace)  run bench_trace 900 python bench.py --workload trace --steps 3 --warmup 1 ;;
