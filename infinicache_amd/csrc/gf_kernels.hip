@@ -99,7 +99,7 @@ struct GenericArgs {
     uint32_t out_off[kMaxRG];
 };
 
-template <int R, int G>
+template <int R, int G, bool PIPE>
 __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
@@ -129,17 +129,50 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
 #pragma unroll
             for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
     };
-    uint32_t c = 0;
-    for (; c + G <= a.K; c += G) {
-        u32x4 x[G];
+    if (!PIPE) {  // one group at a time (R > 4: VALU-bound; the pipeline's
+                  // extra 16 VGPRs cost more waves than its loads gain)
+        uint32_t c = 0;
+        for (; c + G <= a.K; c += G) {
+            u32x4 x[G];
 #pragma unroll
-        for (int g = 0; g < G; ++g)
-            x[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c + g] * a.pitch, kLoadAux);
+            for (int g = 0; g < G; ++g)
+                x[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c + g] * a.pitch, kLoadAux);
 #pragma unroll
-        for (int g = 0; g < G; ++g) mac_input(x[g], c + g);
+            for (int g = 0; g < G; ++g) mac_input(x[g], c + g);
+        }
+        for (; c < a.K; ++c)
+            mac_input(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux), c);
+    } else {
+    // Software pipeline over groups of G inputs: group g+1's loads are issued
+    // before group g is coded, so a wave keeps 2G loads in flight.  Every load
+    // is unconditional (past the last input it goes through a zero-record
+    // resource: no memory traffic), so the wait counts stay static; the row
+    // table is padded on the host for the over-reach.
+    const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, 0, 0x00020000);
+    auto load_group = [&](u32x4(&x)[G], uint32_t g) {
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const uint32_t c = g * G + i;
+            x[i] = __builtin_amdgcn_raw_buffer_load_b128(c < a.K ? rs : rsn, voff, rows[c] * a.pitch, kLoadAux);
+        }
+        asm volatile("" ::: "memory");  // issue here: not sunk into the guarded uses below
+    };
+    auto mac_group = [&](const u32x4(&x)[G], uint32_t g) {
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+            if (g * G + i < a.K) mac_input(x[i], g * G + i);
+    };
+    const uint32_t ng = (a.K + G - 1) / G;
+    u32x4 xa[G], xb[G];
+    load_group(xa, 0);
+    for (uint32_t g = 0; g < ng; g += 2) {
+        load_group(xb, g + 1);
+        mac_group(xa, g);
+        if (g + 1 >= ng) break;
+        load_group(xa, g + 2);
+        mac_group(xb, g + 1);
     }
-    for (; c < a.K; ++c)
-        mac_input(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux), c);
+    }
     bool mismatch = false;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -421,7 +454,9 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     // upload the [K][R][kTabWords] table image and row indices once per plan
     hipError_t e = hipSuccess;
     std::call_once(p.dev_once, [&] {
-        std::vector<uint32_t> t((size_t)K * p.R * kTabWords), rows(K);
+        // rows padded by 3 groups: the pipelined loop's loads reach up to two
+        // groups past the last input (through a zero-record resource)
+        std::vector<uint32_t> t((size_t)K * p.R * kTabWords), rows(K + 3 * kGroup, 0);
         for (int c = 0; c < K; ++c) {
             rows[c] = (uint32_t)p.in_rows[c];
             for (int r = 0; r < p.R; ++r)
@@ -465,7 +500,10 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
         // full occupancy: the wide generic passes are VALU-bound (tools/kbench
         // lib:SHAPE with caps of 2/4/6 workgroups per CU: -8/-1/+0.8 points)
-        hipLaunchKernelGGL((gf_apply_generic<R, kGroup>), dim3(grid), dim3(kBlock), 0, st, a);
+        // pipelined input groups for R <= 4 (tools/kbench lib:SHAPE, cold:
+        // RS(20+4) encode 65.9 -> 68.0 %, decode 64.8 -> 66.1 %; R = 8 shapes
+        // lost 2-3 points to the extra VGPRs, so they keep one group at a time)
+        hipLaunchKernelGGL((gf_apply_generic<R, kGroup, (R <= 4)>), dim3(grid), dim3(kBlock), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
