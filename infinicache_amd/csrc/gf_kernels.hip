@@ -207,13 +207,13 @@ size_t rows_extent(const Plan &p, size_t pitch) {
 
 
 template <int K, int R>
-void fill_pass(const Plan &p, const Sub &s, size_t pitch, uint32_t nvec, bool have_bad, Pass<K, R> &a) {
+void fill_pass(const Plan &p, const Sub &s, size_t pitch, size_t space, uint32_t nvec, bool have_bad, Pass<K, R> &a) {
     a.nw = (uint32_t)s.nw;
     // identity inputs feed the plan's last ki rows; usable only when this
     // pass is the plan's last pass (it holds those rows at the same offsets)
     a.ki = (s.r0 + R == p.R) ? (uint32_t)std::min(p.ki, R) : 0u;
     a.clear = (have_bad && p.nw == p.R) ? 1u : 0u;
-    a.packed = tail_part(pitch, nvec);
+    a.packed = tail_part(space, nvec);
     a.sub_stride = a.sub_len = a.sub_n = 0;
     int maxrow = 0;
     for (int c = 0; c < K; ++c) {
@@ -238,7 +238,7 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
     a.obj_stride = L.obj_stride;
     a.nvec = (uint32_t)((L.shard_len + 15) / 16);
     a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
-    fill_pass<K, R>(p, s, L.pitch, a.nvec, d_bad != nullptr, a.p);
+    fill_pass<K, R>(p, s, L.pitch, row_space(L), a.nvec, d_bad != nullptr, a.p);
     a.p.sub_stride = L.sub_stride;
     a.p.sub_len = L.sub_len;
     a.p.sub_n = L.sub_n;
@@ -319,7 +319,8 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
     for (size_t i = 0; i < es.size(); ++i) {
         // the pass image depends on (plan, pitch, sub-pass, flags): cache it in the plan
         Plan &pl = const_cast<Plan &>(*es[i]->plan);
-        const std::array<uint64_t, 3> key{L.pitch * 2 + (d_bad != nullptr), (uint64_t)es[i]->sub.r0, nvec};
+        const std::array<uint64_t, 3> key{L.pitch * 2 + (d_bad != nullptr), (uint64_t)es[i]->sub.r0,
+                                          (uint64_t)row_space(L) << 32 | nvec};
         const std::vector<uint8_t> *cached = nullptr;
         {
             std::lock_guard<std::mutex> g(pl.img_mu);
@@ -327,7 +328,7 @@ std::function<hipError_t(const uint8_t *dimg, hipStream_t)> stage_class(
                 if (kv.first == key && kv.second.size() == sizeof(Pass<K, R>)) cached = &kv.second;
             if (!cached) {
                 Pass<K, R> pp;
-                fill_pass<K, R>(pl, es[i]->sub, L.pitch, nvec, d_bad != nullptr, pp);
+                fill_pass<K, R>(pl, es[i]->sub, L.pitch, row_space(L), nvec, d_bad != nullptr, pp);
                 std::vector<uint8_t> b(sizeof(pp));
                 std::memcpy(b.data(), &pp, sizeof(pp));
                 if (pl.pass_imgs.size() > 16) pl.pass_imgs.clear();
@@ -480,7 +481,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     a.tab = p.d_tab + (size_t)s.r0 * kTabWords;
     a.in_row = p.d_in_row;
     a.pitch = (uint32_t)L.pitch;
-    a.packed = tail_part(L.pitch, a.nvec);
+    a.packed = tail_part(row_space(L), a.nvec);
     int maxrow = 0;
     for (int c = 0; c < K; ++c) maxrow = std::max(maxrow, p.in_rows[c]);
     for (int r = 0; r < R; ++r) {

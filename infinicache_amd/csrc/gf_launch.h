@@ -71,6 +71,14 @@ inline uint32_t tail_part(size_t pitch, uint32_t nvec) {
     return w < 16 ? (uint32_t)w : 0u;
 }
 
+// Bytes a row of one object may be written up to (store_row's `part`): the
+// row pitch, except in a shard-major layout ([shard][object], obj_stride <
+// pitch), where an object's piece of a row is obj_stride bytes and the next
+// object's piece (or, for the row's last object, the next row) follows.
+inline size_t row_space(const Layout &L) {
+    return L.obj_stride > 0 && L.obj_stride < L.pitch ? L.obj_stride : L.pitch;
+}
+
 // bytes covered by `no` objects of layout L (one object: its own span)
 inline size_t objs_span(const Layout &L, int no, size_t one) {
     return no > 1 ? (size_t)no * L.obj_stride : one;

@@ -90,11 +90,14 @@ def test_shard_major_encode_verify_decode(gpu, k, p, S, nobj, aligned):
         assert torch.equal(_pieces(rows, i, nobj, S, stride), golden[i]), i
 
 
-def test_shard_major_tight_pitch_last_object(gpu):
+@pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 103, 1001), (16, 2, 1, 988), (10, 2, 5, 777), (4, 4, 17, 301)])
+def test_shard_major_tight_pitch_last_object(gpu, k, p, S, nobj):
     """pitch = (nobj-1)*stride + S exactly: the last object's piece ends the
     row, its last 16-B vector would read past the batch; it is coded through
-    the scratch copy (and the conversion to one object is not taken)."""
-    k, p, S, nobj = 10, 2, 103, 1001
+    the scratch copy (and the conversion to one object is not taken).  Pieces
+    narrower than a vector (S = 1, 5): a piece's last vector may only be
+    written up to the piece's end (obj_stride), never into the next object's
+    piece or, at a row's end, into the next row (found by the soak)."""
     n = k + p
     stride = S
     pitch = (nobj - 1) * stride + S

@@ -10,7 +10,10 @@ than tests/test_gpu_random.py:
     flags after random corruption, fused decode (uniform pattern), mixed
     per-object patterns, ReconstructData; shard sizes from 1 B (packed
     small-object workgroups) to 40 KB, gaps between objects;
-  * pinned Split buffers (zero-copy passes) for every per-object op.
+  * pinned Split buffers (zero-copy passes) for every per-object op;
+  * round 2: narrow pitches (down to byte-packed rows), device-resolved mixed
+    patterns (present masks in HBM, every status value), shard-major batches
+    (encode vs the oracle, per-object Verify flags, fused decode).
 Every result is compared bit-exact (bytes) or exactly (booleans, error
 classes) with the oracle on the same input.  Prints a per-kind case count."""
 import collections
@@ -99,7 +102,10 @@ def _device_case(rng, counts):
     p = int(rng.integers(1, 9))
     n = k + p
     S = _size(rng, 40000)
-    pitch = (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+    if rng.random() < 0.25:  # narrow pitch (< 16 * ceil(S / 16)): partial tail stores
+        pitch = (S + 3) // 4 * 4 if rng.random() < 0.5 else S
+    else:
+        pitch = (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
     gap = 16 * int(rng.integers(0, 8))
     stride = n * pitch + gap
     nobj = int(rng.integers(1, max(2, min(400, (24 << 20) // stride))))
@@ -169,6 +175,118 @@ def _device_case(rng, counts):
     assert np.array_equal(out[:, n * pitch:], got[:, n * pitch:]), tag
 
 
+def _masks_case(rng, counts):
+    """Device-resolved mixed patterns: every object its own present mask
+    (too few shards, an extra present parity shard corrupted, all present),
+    decode / reconstruct / data-only; rebuilt rows vs the coded batch."""
+    import torch
+    k = int(rng.integers(1, 15))
+    p = int(rng.integers(1, min(8, 16 - k) + 1))
+    n = k + p
+    S = _size(rng, 30000)
+    pitch = (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 2))
+    stride = n * pitch + 16 * int(rng.integers(0, 4))
+    nobj = int(rng.integers(1, max(2, min(300, (16 << 20) // stride))))
+    op = str(rng.choice(["decode", "reconstruct", "rdata"]))
+    counts["masks_" + op] += 1
+    enc = ia.New(k, p)
+    host = rng.integers(0, 256, (nobj, stride), dtype=np.uint8)
+    for i in range(n):
+        host[:, i * pitch + S:(i + 1) * pitch] = 0
+    buf = torch.from_numpy(host).cuda()
+    st = torch.cuda.current_stream()
+    enc.encode_dev(buf, S, pitch, stride, nobj, st)
+    torch.cuda.synchronize()
+    coded = buf.cpu().numpy()
+    got = coded.copy()
+    pres = np.ones((nobj, n), dtype=np.uint8)
+    want_status = np.zeros(nobj, np.int64)
+    for o in range(nobj):
+        nl = int(rng.integers(0, p + 2))  # p + 1: too few shards
+        pres[o, rng.choice(n, min(nl, n), replace=False)] = 0
+        if pres[o].sum() < k:
+            want_status[o] = 2
+            continue
+        for i in np.flatnonzero(pres[o] == 0):
+            got[o, i * pitch:i * pitch + S] = rng.integers(0, 256, S, dtype=np.uint8)
+        last = int(np.nonzero(pres[o])[0][-1])
+        if op == "decode" and pres[o].sum() > k and last >= k and rng.random() < 0.3:
+            got[o, last * pitch + int(rng.integers(0, S))] ^= 0x24  # an extra (checked) shard
+            want_status[o] = 1
+    masks = (pres.astype(np.int64) << np.arange(n)).sum(axis=1).astype(np.int32)
+    buf = torch.from_numpy(got.copy()).cuda()
+    status = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    dm = torch.from_numpy(masks).cuda()
+    if op == "decode":
+        enc.decode_dev_masks(buf, dm, S, pitch, stride, nobj, status, st)
+    else:
+        enc.reconstruct_dev_masks(buf, dm, S, pitch, stride, nobj, data_only=op == "rdata", status=status,
+                                  stream=st)
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    tag = ("masks", op, k, p, S, pitch, nobj)
+    assert np.array_equal(status.cpu().numpy(), want_status), tag
+    for o in range(nobj):
+        if want_status[o] == 2:
+            assert np.array_equal(out[o], got[o]), tag
+            continue
+        for i in range(n):
+            a = out[o, i * pitch:i * pitch + S]
+            if pres[o, i] or (op == "rdata" and i >= k):
+                assert np.array_equal(a, got[o, i * pitch:i * pitch + S]), (tag, o, i)
+            else:
+                assert np.array_equal(a, coded[o, i * pitch:i * pitch + S]), (tag, o, i)
+
+
+def _shard_major_case(rng, counts):
+    """[shard][object] batches: encode vs the oracle (the batch is one long
+    object per row), Verify flags per object, fused decode."""
+    import torch
+    k = int(rng.integers(1, 21))
+    p = int(rng.integers(1, 7))
+    n = k + p
+    S = _size(rng, 5000)
+    ostride = S if rng.random() < 0.5 else (S + 15) // 16 * 16
+    nobj = int(rng.integers(2, max(3, min(3000, (8 << 20) // (n * ostride)))))
+    pitch = nobj * ostride + 16 * int(rng.integers(0, 3))
+    counts["shardmajor"] += 1
+    enc = ia.New(k, p)
+    m = enc.matrix()
+    host = np.zeros((n, pitch), np.uint8)
+    for i in range(k):
+        host[i, :nobj * ostride].reshape(nobj, ostride)[:, :S] = rng.integers(0, 256, (nobj, S), dtype=np.uint8)
+    buf = torch.from_numpy(host.copy()).cuda()
+    st = torch.cuda.current_stream()
+    enc.encode_dev(buf, S, pitch, ostride, nobj, st)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    piece = lambda a, i: a[i, :nobj * ostride].reshape(nobj, ostride)[:, :S]
+    want = oracle.apply(m[k:], [piece(host, i).reshape(-1) for i in range(k)])
+    tag = ("shardmajor", k, p, S, ostride, nobj)
+    for r in range(p):
+        assert np.array_equal(piece(got, k + r).reshape(-1), want[r]), tag
+    hit = sorted(set(rng.integers(0, nobj, int(rng.integers(0, 5))).tolist()))
+    bad_in = got.copy()
+    for o in hit:
+        piece(bad_in, int(rng.integers(0, n)))[o, int(rng.integers(0, S))] ^= 0x42
+    bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    enc.verify_dev(torch.from_numpy(bad_in).cuda(), S, pitch, ostride, nobj, bad, st)
+    torch.cuda.synchronize()
+    assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit, tag
+    lost = sorted(rng.choice(n, int(rng.integers(1, p + 1)), replace=False).tolist())
+    erased = got.copy()
+    for i in lost:
+        piece(erased, i)[:] = 0xA5
+    buf = torch.from_numpy(erased).cuda()
+    bad.fill_(9)
+    enc.decode_dev(buf, [i not in lost for i in range(n)], S, pitch, ostride, nobj, bad, st)
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    assert not bad.any(), tag
+    for i in range(n):
+        assert np.array_equal(piece(out, i), piece(got, i)), (tag, lost, i)
+
+
 def _call(enc, fn, bufs, lens, *extra):
     n = len(bufs)
     from infinicache_amd import _lib
@@ -236,10 +354,14 @@ def test_gpu_soak_vs_oracle(gpu):
     t0 = last = time.time()
     while time.time() - t0 < SECONDS:
         r = rng.random()
-        if r < 0.4:
+        if r < 0.3:
             _host_case(rng, counts)
-        elif r < 0.75:
+        elif r < 0.55:
             _device_case(rng, counts)
+        elif r < 0.7:
+            _masks_case(rng, counts)
+        elif r < 0.85:
+            _shard_major_case(rng, counts)
         else:
             _pinned_case(rng, counts)
         if time.time() - last > 30:  # progress line (a silent GPU run reads as hung)

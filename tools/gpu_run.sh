@@ -22,6 +22,7 @@ STEPS=${STEPS:-"pytest smoke bench prof"}
 for s in $STEPS; do
   case $s in
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    soak)   RSGPU_SOAK_SECONDS=${SOAK_SECONDS:-240} RSGPU_SOAK_SEED=${SOAK_SEED:-20261016} run soak $(( ${SOAK_SECONDS:-240} + 240 )) python -u -m pytest tests/test_gpu_soak.py -m gpu -x -s --timeout $(( ${SOAK_SECONDS:-240} + 200 )) --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ;;
     bench_all)
