@@ -29,6 +29,7 @@ for s in $STEPS; do
             run bench_enc 300 python bench.py --workload enc --no-cpu
             run bench_dec4 300 python bench.py --workload dec4 --no-cpu
             run bench_mixed 300 python bench.py --workload encdec_mixed --no-cpu ;;
+    shardmajor) run pytest_shardmajor 600 python -u -m pytest tests/test_gpu_shardmajor.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     masks)  run pytest_masks 600 python -u -m pytest tests/test_gpu_masks.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     mixed)  for wl in small_mixed encdec_mixed small; do
               run bench_$wl 300 python bench.py --workload $wl --no-cpu
