@@ -85,7 +85,16 @@ Plan::~Plan() {
 // kMaxRG = 8 rows per pass: runtime input loop over groups of G inputs whose
 // G loads are issued together (memory-level parallelism inside the wave),
 // tables and row indices read with scalar loads from a device image
-// [K][rstride][kTabWords] (constant address space: s_load).
+// [K][rstride][kTabWords] (constant address space: s_load).  The wide passes
+// are VALU-bound, so the math is trimmed (tools/kbench lib:SHAPE, cold,
+// profiles/r02_kbench_lib_generic_pair_ldst.txt; RS(32+8) encode 48.8 ->
+// 55.0 %, RS(64+16) 23.5 -> 27.5 %):
+//   * inputs go in pairs: their 6 lookups fold into an accumulator with 3
+//     xor3 (one input alone: an xor3 and an xor for its 3 lookups);
+//   * the table words v_perm needs in VGPRs (t[1], t[3]: one operand of each
+//     8-entry lookup; GFX9's constant bus gives the other its SGPR) are staged
+//     in LDS once per workgroup and read as one broadcast ds_read_b64 per
+//     (input, row), instead of two v_mov per (input, row).
 constexpr int kMaxRG = 8;
 constexpr int kGroup = 4;
 struct GenericArgs {
@@ -103,6 +112,13 @@ template <int R, int G, bool PIPE>
 __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
+    extern __shared__ u32x2 lvw[];  // [K][R]: table words 1 and 3 (dynamic LDS, K * R * 8 B)
+    for (uint32_t i = threadIdx.x; i < a.K * R; i += kBlock) {
+        const uint32_t c = i / R, r = i - c * R;
+        const uint32_t *e = a.tab + ((size_t)c * a.rstride + r) * kTabWords;
+        lvw[i] = u32x2{e[1], e[3]};
+    }
+    __syncthreads();
     const uint32_t v = chunk * kBlock + threadIdx.x;
     if (v >= a.nvec) return;
     const uint8_t *ob = a.base + (uint64_t)obj * a.obj_stride;
@@ -129,6 +145,27 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
 #pragma unroll
             for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
     };
+    // inputs c and c + 1 together (see above)
+    auto mac_pair = [&](const u32x4 &xa, const u32x4 &xb, uint32_t c) {
+        const constant_ptr<uint32_t> ta = tab + (size_t)c * a.rstride * kTabWords;
+        const constant_ptr<uint32_t> tb = ta + (size_t)a.rstride * kTabWords;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const GfIdx ga = gf_idx(xa[d]), gb = gf_idx(xb[d]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const constant_ptr<uint32_t> A = ta + r * kTabWords, B = tb + r * kTabWords;
+                const u32x2 wa = lvw[c * R + r], wb = lvw[(c + 1) * R + r];
+                uint32_t s = xor3(acc[r][d], lut8(A[0], wa[0], ga.i0), lut8(A[2], wa[1], ga.i1));
+                s = xor3(s, lut8(A[4], A[4], ga.i2), lut8(B[0], wb[0], gb.i0));
+                acc[r][d] = xor3(s, lut8(B[2], wb[1], gb.i1), lut8(B[4], B[4], gb.i2));
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+    };
     if (!PIPE) {  // one group at a time (R > 4: VALU-bound; the pipeline's
                   // extra 16 VGPRs cost more waves than its loads gain)
         uint32_t c = 0;
@@ -138,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
             for (int g = 0; g < G; ++g)
                 x[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c + g] * a.pitch, kLoadAux);
 #pragma unroll
-            for (int g = 0; g < G; ++g) mac_input(x[g], c + g);
+            for (int g = 0; g < G; g += 2) mac_pair(x[g], x[g + 1], c + g);
         }
         for (; c < a.K; ++c)
             mac_input(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux), c);
@@ -159,8 +196,10 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     };
     auto mac_group = [&](const u32x4(&x)[G], uint32_t g) {
 #pragma unroll
-        for (int i = 0; i < G; ++i)
-            if (g * G + i < a.K) mac_input(x[i], g * G + i);
+        for (int i = 0; i < G; i += 2) {
+            if (g * G + i + 1 < a.K) mac_pair(x[i], x[i + 1], g * G + i);
+            else if (g * G + i < a.K) mac_input(x[i], g * G + i);
+        }
     };
     const uint32_t ng = (a.K + G - 1) / G;
     u32x4 xa[G], xb[G];
@@ -504,7 +543,8 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         // pipelined input groups for R <= 4 (tools/kbench lib:SHAPE, cold:
         // RS(20+4) encode 65.9 -> 68.0 %, decode 64.8 -> 66.1 %; R = 8 shapes
         // lost 2-3 points to the extra VGPRs, so they keep one group at a time)
-        hipLaunchKernelGGL((gf_apply_generic<R, kGroup, (R <= 4)>), dim3(grid), dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL((gf_apply_generic<R, kGroup, (R <= 4)>), dim3(grid), dim3(kBlock), (unsigned)(K * R * 8),
+                           st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
