@@ -292,11 +292,20 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
     }
 }
 
-template <int K, int R, int U, int BS, int LAUX, int SAUX>
+// FORM: which launch shapes one instantiation serves.  Each form is its own
+// kernel so that its register allocation is its own: with every form in one
+// kernel the 100 table words no longer fit the SGPR file beside the other
+// forms' uniforms, and the compiler parks them in VGPR lanes (80 v_writelane
+// per wave, plus 92 v_readlane per wave in the small-object form).
+constexpr int kFormAny = 0;       // runtime: small objects if a.opw > 1, else chunks (+ redirection)
+constexpr int kFormChunks = 1;    // one object per workgroup chunk, no redirection
+constexpr int kFormSmall = 2;     // a.opw > 1 objects per workgroup
+constexpr int kFormRedirect = 3;  // one object, zero-copy redirection (per-object host API)
+template <int K, int R, int U, int BS, int LAUX, int SAUX, int FORM = kFormAny>
 __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
-    if (a.opw > 1) {  // small objects: lane -> (object j of the group, vector v)
+    if (FORM == kFormSmall || (FORM == kFormAny && a.opw > 1)) {  // small objects: lane -> (object j of the group, vector v)
         const uint32_t j = threadIdx.x / a.nvec, o0 = obj * a.opw;
         if (j >= a.opw || o0 + j >= a.nobj) return;
         gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)o0 * a.obj_stride, o0 + j, a.p, a.nvec,
@@ -305,11 +314,13 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
         return;
     }
     Redirect rd;
-    rd.in = a.in_base;
-    rd.in_span = a.in_span;
-    rd.copy_in = a.copy_in != 0;
-    rd.out = a.out_base;
-    rd.dual = a.out_dual != 0;
+    if (FORM == kFormAny || FORM == kFormRedirect) {
+        rd.in = a.in_base;
+        rd.in_span = a.in_span;
+        rd.copy_in = a.copy_in != 0;
+        rd.out = a.out_base;
+        rd.dual = a.out_dual != 0;
+    }
     gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec,
                                            a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd);
 }

@@ -308,8 +308,8 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
                 // ~1 KiB of consecutive rows measured +6 points at 1 KiB
                 // encode, 0 on decode and -7 / -4 points at 4 / 16 KiB:
                 // tools/kbench KB_SET=small, not shipped)
-                hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
-                                   dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
+                hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormSmall>),
+                                   dim3(grid), dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
                 hipError_t e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -328,8 +328,12 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
         a.bad = d_bad ? d_bad + o0 : nullptr;
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
-        hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux>), dim3(grid),
-                           dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
+        if (L.in_base || L.out_base)
+            hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormRedirect>),
+                               dim3(grid), dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
+        else
+            hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormChunks>),
+                               dim3(grid), dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
