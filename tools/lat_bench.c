@@ -1,10 +1,11 @@
 /* lat_bench.c — per-object latency of the host-buffer C ABI, as the cgo shim
  *  drives it for one EcSet / EcGet: Client.encode = Encode +
  * Verify (separate calls, and fused: rsgpu_encode_verify), Client.decode =
- * Reconstruct + Verify (fused, rsgpu_decode), 1 MiB
- * RS(10+2) objects, shards as Split lays them out (one contiguous buffer).
+ * Reconstruct + Verify (fused, rsgpu_decode), RS(10+2) objects of
+ * LAT_BYTES bytes (default 1 MiB; client/example/main.go uses 1 KiB), shards
+ * as Split lays them out (one contiguous buffer).
  *
- *   ./lat_bench [iters]
+ *   [LAT_BYTES=N] ./lat_bench [iters [concurrent_seconds]]
  *
  * Prints p50/p99 in microseconds for pageable (malloc) and pinned
  * (rsgpu_host_alloc) buffers.  No Python in the process. */
@@ -29,6 +30,11 @@ static int cmp(const void *a, const void *b) {
     return x < y ? -1 : x > y;
 }
 
+static size_t obj_bytes(void) {
+    const char *e = getenv("LAT_BYTES");
+    return e && atol(e) > 0 ? (size_t)atol(e) : (size_t)1 << 20;
+}
+
 static double pct(double *v, int n, double p) {
     qsort(v, n, sizeof(double), cmp);
     int i = (int)(p * (n - 1) + 0.5);
@@ -49,7 +55,7 @@ struct conc_arg {
 static void *conc_worker(void *vp) {
     struct conc_arg *a = (struct conc_arg *)vp;
     const int k = 10, p = 2, n = k + p;
-    const size_t nb = 1 << 20, S = (nb + k - 1) / k;
+    const size_t nb = obj_bytes(), S = (nb + k - 1) / k;
     uint8_t *buf = NULL;
     if (rsgpu_host_alloc(n * S, (void **)&buf)) { a->err = 1; return NULL; }
     for (size_t i = 0; i < k * S; ++i) buf[i] = (uint8_t)(i * 131 + 7);
@@ -87,7 +93,7 @@ static int concurrent(rsgpu_ctx *ctx, int threads, double secs) {
     }
     const double el = (now_us() - t0) * 1e-6;
     printf("concurrent %2d threads: %7.0f objects/s (encode+verify and decode each), %6.2f GiB/s of object "
-           "bytes per op pair%s\n", threads, done / el, 2.0 * done * (1 << 20) / el / (1 << 30),
+           "bytes per op pair%s\n", threads, done / el, 2.0 * done * (double)obj_bytes() / el / (1 << 30),
            err ? "  ERROR" : "");
     return err;
 }
@@ -95,8 +101,9 @@ static int concurrent(rsgpu_ctx *ctx, int threads, double secs) {
 int main(int argc, char **argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 200, warm = 10;
     const int k = 10, p = 2, n = k + p;
-    const size_t nb = 1 << 20, S = (nb + k - 1) / k;
+    const size_t nb = obj_bytes(), S = (nb + k - 1) / k;
     rsgpu_ctx *ctx;
+    printf("object %zu B (S = %zu)\n", nb, S);
     if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
     double *te = malloc(sizeof(double) * iters), *td = malloc(sizeof(double) * iters);
     double *tf = malloc(sizeof(double) * iters);
