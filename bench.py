@@ -56,6 +56,15 @@ WORKLOADS = {
     "small1k_p1": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
                        palign=1, desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, "
                                       "byte-packed rows (pitch 103)"),
+    # rows padded to whole 64/128-B sectors: every row piece is read and
+    # written as whole sectors (no partial-sector writes), at the cost of
+    # the padding bytes
+    "small1k_p128": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
+                         palign=128, desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, pitch 128"),
+    "small_p64": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
+                      palign=64, desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, pitch 448"),
+    "small_p128": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
+                       palign=128, desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, pitch 512"),
     # shard-major batches ([shard][object]: shard i of all objects back to
     # back, as InfiniCache ships shard i to Lambda node i): the batch is coded
     # as one object per shard row, whatever the object size
@@ -105,6 +114,9 @@ METRICS = {
     "small_sm": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch), 4 KiB objects",
     "small1k_p4": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
     "small1k_p1": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
+    "small1k_p128": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
+    "small_p64": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
+    "small_p128": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
     "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
 }
 
