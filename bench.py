@@ -77,6 +77,11 @@ WORKLOADS = {
                              desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, shard-major "
                                   "(16-B aligned pieces), per-object random erasure pair (device-resident "
                                   "present masks)"),
+    "small1k_sm_mixed_a128": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
+                                  shard_major=True, oalign=128, mixed=True,
+                                  desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, shard-major "
+                                       "(128-B aligned pieces: one line each), per-object random erasure pair "
+                                       "(device-resident present masks)"),
     "small_sm": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
                      shard_major=True, oalign=1,
                      desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, shard-major"),
@@ -111,6 +116,8 @@ METRICS = {
     "small1k_sm": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch), 1 KiB objects",
     "small1k_sm_mixed": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch, mixed erasure "
                         "patterns), 1 KiB objects",
+    "small1k_sm_mixed_a128": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch, mixed erasure "
+                             "patterns), 1 KiB objects",
     "small_sm": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch), 4 KiB objects",
     "small1k_p4": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
     "small1k_p1": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",

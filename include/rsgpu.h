@@ -158,17 +158,25 @@ int rsgpu_decode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nsha
 
 /* ---- batched device-resident API (HBM in, HBM out) ---------------------
  * Layout: shard i of object o lives at d_base + o*obj_stride + i*pitch, for
- * i in [0, data+parity).  Requirements: pitch >= shard_len, obj_stride >=
- * (data+parity)*pitch when nobj > 1, and (data+parity)*pitch < 4 GiB; any
- * alignment (16-B aligned d_base, pitch and obj_stride are the fast path and
- * are required by the *_dev_masks calls).  Kernels read whole 16-B vectors
- * and write them where the row's pitch allows: written rows' bytes in
- * [shard_len, min(pitch, roundup16(shard_len))) are overwritten with the
- * coding of the input rows' pad bytes (zero when those are zero); with a
- * pitch below roundup16(shard_len) (e.g. pitch = shard_len, byte-packed rows)
- * nothing past shard_len is written.  `stream` is a hipStream_t (NULL =
- * default stream); calls are asynchronous on it and make no host<->device
- * synchronisation. */
+ * i in [0, data+parity), in either orientation:
+ *   object-major ([object][shard]): obj_stride >= (data+parity)*pitch when
+ *     nobj > 1, pitch >= shard_len;
+ *   shard-major ([shard][object], each shard row holds every object's piece):
+ *     shard_len <= obj_stride and pitch >= (nobj-1)*obj_stride + shard_len.
+ *     A batch whose gaps between pieces are narrow (obj_stride <=
+ *     roundup16(shard_len), or a gap of at most shard_len/4) is coded as one
+ *     object whose shard is the whole row: the gap bytes are pad bytes and
+ *     are overwritten in written rows, as are the row's bytes up to
+ *     roundup16 of its last piece's end when the pitch holds them.
+ * (data+parity)*pitch < 4 GiB; any alignment (16-B aligned d_base, pitch and
+ * obj_stride are the fast path and are required by the *_dev_masks calls).
+ * Kernels read whole 16-B vectors and write them where the layout allows:
+ * written rows' bytes in [shard_len, min(space, roundup16(shard_len))), space
+ * = the pitch (object-major) or obj_stride (shard-major), are overwritten
+ * with the coding of the input rows' pad bytes (zero when those are zero);
+ * with less space (e.g. pitch = shard_len, byte-packed rows) nothing past
+ * shard_len is written.  `stream` is a hipStream_t (NULL = default stream);
+ * calls are asynchronous on it and make no host<->device synchronisation. */
 
 /* Encode nobj objects: rows [k, k+p) <- M[k:] x rows [0, k). */
 int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitch,

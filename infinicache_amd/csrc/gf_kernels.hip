@@ -624,13 +624,16 @@ hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
     // base + i*pitch + o*obj_stride, the objects' pieces of one shard back to
     // back): coding is byte-position-wise, so the batch IS one object whose
     // shard is the whole row, streamed at the large-object rate however small
-    // the objects are.  Gaps between pieces (obj_stride up to roundup16(S))
-    // are pad bytes.  Check flags stay per object (Pass::sub_*); the generic
-    // kernel (K > 16) has no per-object attribution, so it converts only
-    // without flags.
+    // the objects are.  Gaps between pieces are pad bytes, coded along (and
+    // overwritten in written rows): taken while a gap is at most
+    // roundup16(S) - S or a quarter of S (1 KiB objects at a 128-B stride,
+    // whole-line pieces); wider gaps go object by object.  Check flags stay
+    // per object (Pass::sub_*); the generic kernel (K > 16) has no per-object
+    // attribution, so it converts only without flags.
     const size_t row = (size_t)(L.nobj - 1) * L.obj_stride + L.shard_len;
+    const bool narrow_gaps = L.obj_stride <= (L.shard_len + 15) / 16 * 16 || (L.obj_stride - L.shard_len) * 4 <= L.shard_len;
     if (L.nobj > 1 && !L.in_base && !L.out_base && L.sub_stride == 0 && L.obj_stride >= L.shard_len &&
-        L.obj_stride <= (L.shard_len + 15) / 16 * 16 && (row + 15) / 16 * 16 <= L.pitch &&
+        narrow_gaps && (row + 15) / 16 * 16 <= L.pitch &&
         (p.K <= kMaxK || !d_bad) && (size_t)L.nobj * L.obj_stride < ((size_t)1 << 32)) {
         Layout big{L.base, 0, L.pitch, row, 1};
         big.slack = L.slack;

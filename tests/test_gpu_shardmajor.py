@@ -90,6 +90,47 @@ def test_shard_major_encode_verify_decode(gpu, k, p, S, nobj, aligned):
         assert torch.equal(_pieces(rows, i, nobj, S, stride), golden[i]), i
 
 
+@pytest.mark.parametrize("k,p,S,stride,nobj", [(10, 2, 103, 128, 3000), (10, 2, 100, 128, 2000), (10, 4, 410, 512, 700),
+                                               (20, 4, 103, 128, 500)])
+def test_shard_major_wide_gaps(gpu, k, p, S, stride, nobj):
+    """Pieces at a stride past roundup16(S): gaps up to S/4 are coded along
+    as pad bytes (one-object conversion: 103 -> 128, 410 -> 512), wider ones
+    (100 -> 128) object by object; parity, per-object Verify flags (garbage in
+    the gaps is not a mismatch) and fused decode against the oracle."""
+    n = k + p
+    pitch = (nobj * stride + 255) // 256 * 256
+    flat, rows = _batch(k, p, S, nobj, stride, pitch, seed=S + stride + nobj)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    before = rows.clone()
+    enc.encode_dev(flat, S, pitch, stride, nobj, s)
+    torch.cuda.synchronize()
+    want = _expect_parity(enc, before, k, p, nobj, S, stride)
+    for r in range(p):
+        assert np.array_equal(_pieces(rows, k + r, nobj, S, stride).cpu().numpy().reshape(-1), want[r]), r
+    assert torch.equal(rows[:k], before[:k])
+    rows[:, :nobj * stride].view(n, nobj, stride)[:, ::3, S:] = 0x5D  # garbage in the gaps
+    hit = sorted({1, nobj // 2, nobj - 1})
+    for o in hit:
+        _pieces(rows, (o * 3) % n, nobj, S, stride)[o, (o * 11) % S] ^= 0x81
+    bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    enc.verify_dev(flat, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit
+    for o in hit:
+        _pieces(rows, (o * 3) % n, nobj, S, stride)[o, (o * 11) % S] ^= 0x81
+    golden = [_pieces(rows, i, nobj, S, stride).clone() for i in range(n)]
+    lost = (2, k)
+    for i in lost:
+        _pieces(rows, i, nobj, S, stride).fill_(0x3C)
+    bad.fill_(7)
+    enc.decode_dev(flat, [i not in lost for i in range(n)], S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert not bad.any()
+    for i in range(n):
+        assert torch.equal(_pieces(rows, i, nobj, S, stride), golden[i]), i
+
+
 @pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 103, 1001), (16, 2, 1, 988), (10, 2, 5, 777), (4, 4, 17, 301)])
 def test_shard_major_tight_pitch_last_object(gpu, k, p, S, nobj):
     """pitch = (nobj-1)*stride + S exactly: the last object's piece ends the
