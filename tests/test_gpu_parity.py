@@ -121,9 +121,12 @@ def test_encode_zero_and_ff(gpu):
 @pytest.mark.parametrize("k,p,kind", [(1, 1, "vandermonde"), (3, 13, "vandermonde"),
                                       (4, 2, "cauchy"), (6, 3, "par1"), (10, 6, "vandermonde"),
                                       (16, 4, "vandermonde"), (17, 3, "vandermonde"),
-                                      (20, 4, "cauchy"), (64, 8, "vandermonde")])
+                                      (20, 4, "cauchy"), (64, 8, "vandermonde"), (200, 56, "vandermonde"),
+                                      (128, 128, "cauchy")])
 def test_shapes_and_matrix_kinds(gpu, k, p, kind):
-    """K > 16 takes the generic kernel; R > 4 takes several passes."""
+    """K > 16 takes the generic kernel; R > 4 takes several passes (up to
+    256 shards: Verify codes 256 inputs, the generic kernel's largest LDS
+    table stage)."""
     size = 333
     want = _full(k, p, size, idx=k * 100 + p, kind=kind)
     enc = ia.New(k, p, matrix=kind)
