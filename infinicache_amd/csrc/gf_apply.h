@@ -42,6 +42,7 @@ struct Plan {
     // immutable (safe for concurrent launches)
     uint32_t *d_tab = nullptr;     // [K][R][kCoefWords] (input-major)
     uint32_t *d_in_row = nullptr;  // [K]
+    uint32_t *d_tab3 = nullptr;    // [K/3][R][16] input-triple tables (gf_apply_generic)
     std::once_flag dev_once;
     hipError_t dev_err = hipSuccess;
     // serialized Pass images for mixed-pattern launches, keyed by (pitch and

@@ -79,44 +79,62 @@ int Plan::identity_inputs() const {
 Plan::~Plan() {
     if (d_tab) (void)hipFree(d_tab);
     if (d_in_row) (void)hipFree(d_in_row);
+    if (d_tab3) (void)hipFree(d_tab3);
 }
 
 // Generic pass for K > 16 inputs (any shard count up to 256) and up to
-// kMaxRG = 8 rows per pass: runtime input loop over groups of G inputs whose
-// G loads are issued together (memory-level parallelism inside the wave),
-// tables and row indices read with scalar loads from a device image
-// [K][rstride][kTabWords] (constant address space: s_load).  The wide passes
-// are VALU-bound, so the math is trimmed (tools/kbench lib:SHAPE, cold,
-// profiles/r02_kbench_lib_generic_pair_ldst.txt; RS(32+8) encode 48.8 ->
-// 55.0 %, RS(64+16) 23.5 -> 27.5 %):
-//   * inputs go in pairs: their 6 lookups fold into an accumulator with 3
-//     xor3 (one input alone: an xor3 and an xor for its 3 lookups);
-//   * the table words v_perm needs in VGPRs (t[1], t[3]: one operand of each
-//     8-entry lookup; GFX9's constant bus gives the other its SGPR) are staged
-//     in LDS once per workgroup and read as one broadcast ds_read_b64 per
-//     (input, row), instead of two v_mov per (input, row).
+// kMaxRG = 8 rows per pass: runtime input loop, tables and row indices read
+// with scalar loads from device images (constant address space: s_load).
+// The wide passes are VALU-bound, so the math is trimmed (tools/kbench
+// lib:SHAPE, cold; profiles/r02_kbench_lib_generic_pair_ldst.txt,
+// r02_kbench_generic_triples.txt):
+//   * inputs go in triples: the 24 index bits of inputs a, b, c are eight
+//     3-bit groups, bits [2:0] and [5:3] of each input plus {a[7:6], b[7]}
+//     and {b[6], c[7:6]}, and each group is one v_perm lookup into an
+//     8-entry table of its row (the two cross groups' tables mix two
+//     coefficients).  Per row and dword: 8 v_perm + 4 xor3 for three inputs,
+//     against 9 + 4.5 with three single inputs; selectors 17 ops per three
+//     input dwords, shared by all rows;
+//   * triples are pipelined through their selectors: once a triple's 32
+//     selector words exist its inputs are dead, and the next triple's three
+//     loads go out into those registers while this triple's rows are coded;
+//   * the table words v_perm needs in VGPRs (GFX9's constant bus gives one
+//     operand of each lookup its SGPR, the other must be a VGPR) are staged
+//     in LDS once per workgroup and read as broadcast ds_read_b128;
+//   * K mod 3 leftover inputs go as a pair (6 lookups, 3 xor3) or one input
+//     through the 5-word single-coefficient tables.
 constexpr int kMaxRG = 8;
-constexpr int kGroup = 4;
+constexpr int kRowPad = 8;  // row-index image padding past K (the pipelined loads' over-reach)
 struct GenericArgs {
     const uint8_t *base;
     uint64_t obj_stride;
     uint32_t *bad;
     const uint32_t *tab;     // [K][rstride][kTabWords], pre-offset to this pass's first row
-    const uint32_t *in_row;  // [K] row indices; offset = row * pitch
+    const uint32_t *tab3;    // [K/3][rstride][16] triple tables, pre-offset the same way
+    const uint32_t *in_row;  // [K + kRowPad] row indices; offset = row * pitch
     uint32_t nvec, tail, nw, span, K, rstride, pitch, clear, packed;
     Order ord;  // item = object
     uint32_t out_off[kMaxRG];
 };
 
-template <int R, int G, bool PIPE>
+// LDS: [K][R] u32x2 single-input table words 1 and 3, then [K/3][R][8] high
+// words of the triple tables (generic_lds)
+template <int R>
 __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
-    extern __shared__ u32x2 lvw[];  // [K][R]: table words 1 and 3 (dynamic LDS, K * R * 8 B)
+    extern __shared__ u32x4 lds_tab[];
+    u32x2 *lvw = (u32x2 *)lds_tab;
     for (uint32_t i = threadIdx.x; i < a.K * R; i += kBlock) {
         const uint32_t c = i / R, r = i - c * R;
         const uint32_t *e = a.tab + ((size_t)c * a.rstride + r) * kTabWords;
         lvw[i] = u32x2{e[1], e[3]};
+    }
+    u32x4 *lv3 = lds_tab + (a.K * R + 1) / 2;
+    for (uint32_t i = threadIdx.x; i < a.K / 3 * R * 2; i += kBlock) {
+        const uint32_t tr = i >> 1, t = tr / R, r = tr - t * R;
+        const uint32_t *e = a.tab3 + ((size_t)t * a.rstride + r) * 16 + 8 + (i & 1) * 4;
+        lv3[i] = u32x4{e[0], e[1], e[2], e[3]};
     }
     __syncthreads();
     const uint32_t v = chunk * kBlock + threadIdx.x;
@@ -124,6 +142,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     const uint8_t *ob = a.base + (uint64_t)obj * a.obj_stride;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)a.span, 0x00020000);
+    // loads past the last triple go through a zero-record resource: no memory
+    // traffic, and the wait counts stay static
+    const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, 0, 0x00020000);
     const uint32_t voff = v * 16u;
     const constant_ptr<uint32_t> tab = (constant_ptr<uint32_t>)a.tab;
     const constant_ptr<uint32_t> rows = (constant_ptr<uint32_t>)a.in_row;
@@ -132,6 +153,14 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+    // keep the input-at-a-time order: without these fences the scheduler
+    // hoists every input's index math and splits the work row by row
+    auto fence = [&] {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+    };
     auto mac_input = [&](const u32x4 &x, uint32_t c) {
         const constant_ptr<uint32_t> t = tab + (size_t)c * a.rstride * kTabWords;
 #pragma unroll
@@ -140,12 +169,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], t + r * kTabWords, g);
         }
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+        fence();
     };
-    // inputs c and c + 1 together (see above)
     auto mac_pair = [&](const u32x4 &xa, const u32x4 &xb, uint32_t c) {
         const constant_ptr<uint32_t> ta = tab + (size_t)c * a.rstride * kTabWords;
         const constant_ptr<uint32_t> tb = ta + (size_t)a.rstride * kTabWords;
@@ -161,56 +186,63 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
                 acc[r][d] = xor3(s, lut8(B[2], wb[1], gb.i1), lut8(B[4], B[4], gb.i2));
             }
         }
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+        fence();
     };
-    if (!PIPE) {  // one group at a time (R > 4: VALU-bound; the pipeline's
-                  // extra 16 VGPRs cost more waves than its loads gain)
-        uint32_t c = 0;
-        for (; c + G <= a.K; c += G) {
-            u32x4 x[G];
+    // selectors of one triple (the 8 groups above) for the lane's 4 dwords
+    auto tri_sel = [&](const u32x4 &xa, const u32x4 &xb, const u32x4 &xc, uint32_t (&sel)[4][8]) {
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-                x[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c + g] * a.pitch, kLoadAux);
-#pragma unroll
-            for (int g = 0; g < G; g += 2) mac_pair(x[g], x[g + 1], c + g);
-        }
-        for (; c < a.K; ++c)
-            mac_input(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux), c);
-    } else {
-    // Software pipeline over groups of G inputs: group g+1's loads are issued
-    // before group g is coded, so a wave keeps 2G loads in flight.  Every load
-    // is unconditional (past the last input it goes through a zero-record
-    // resource: no memory traffic), so the wait counts stay static; the row
-    // table is padded on the host for the over-reach.
-    const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, 0, 0x00020000);
-    auto load_group = [&](u32x4(&x)[G], uint32_t g) {
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-            const uint32_t c = g * G + i;
-            x[i] = __builtin_amdgcn_raw_buffer_load_b128(c < a.K ? rs : rsn, voff, rows[c] * a.pitch, kLoadAux);
-        }
-        asm volatile("" ::: "memory");  // issue here: not sunk into the guarded uses below
-    };
-    auto mac_group = [&](const u32x4(&x)[G], uint32_t g) {
-#pragma unroll
-        for (int i = 0; i < G; i += 2) {
-            if (g * G + i + 1 < a.K) mac_pair(x[i], x[i + 1], g * G + i);
-            else if (g * G + i < a.K) mac_input(x[i], g * G + i);
+        for (int d = 0; d < 4; ++d) {
+            sel[d][0] = xa[d] & 0x07070707u;
+            sel[d][1] = (xa[d] >> 3) & 0x07070707u;
+            sel[d][2] = xb[d] & 0x07070707u;
+            sel[d][3] = (xb[d] >> 3) & 0x07070707u;
+            sel[d][4] = xc[d] & 0x07070707u;
+            sel[d][5] = (xc[d] >> 3) & 0x07070707u;
+            sel[d][6] = ((xa[d] >> 5) & 0x06060606u) | ((xb[d] >> 7) & 0x01010101u);
+            sel[d][7] = ((xb[d] >> 6) & 0x01010101u) | ((xc[d] >> 5) & 0x06060606u);
         }
     };
-    const uint32_t ng = (a.K + G - 1) / G;
-    u32x4 xa[G], xb[G];
-    load_group(xa, 0);
-    for (uint32_t g = 0; g < ng; g += 2) {
-        load_group(xb, g + 1);
-        mac_group(xa, g);
-        if (g + 1 >= ng) break;
-        load_group(xa, g + 2);
-        mac_group(xb, g + 1);
+    // triple t into every row: table word w of row r is the SGPR low half
+    // T[r][w] and the LDS high half lv3[t][r][w]
+    auto tri_rows = [&](const uint32_t (&sel)[4][8], uint32_t t) {
+        const constant_ptr<uint32_t> T = (constant_ptr<uint32_t>)a.tab3 + (size_t)t * a.rstride * 16;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const constant_ptr<uint32_t> L = T + r * 16;
+            const u32x4 h0 = lv3[(t * R + r) * 2], h1 = lv3[(t * R + r) * 2 + 1];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                uint32_t q = xor3(acc[r][d], lut8(L[0], h0[0], sel[d][0]), lut8(L[1], h0[1], sel[d][1]));
+                q = xor3(q, lut8(L[2], h0[2], sel[d][2]), lut8(L[3], h0[3], sel[d][3]));
+                q = xor3(q, lut8(L[4], h1[0], sel[d][4]), lut8(L[5], h1[1], sel[d][5]));
+                acc[r][d] = xor3(q, lut8(L[6], h1[2], sel[d][6]), lut8(L[7], h1[3], sel[d][7]));
+            }
+        }
+        fence();
+    };
+    const uint32_t nt = a.K / 3;
+    u32x4 x0, x1, x2;
+    auto load3 = [&](uint32_t c) {
+        const __amdgpu_buffer_rsrc_t r3 = c < nt * 3 ? rs : rsn;
+        x0 = __builtin_amdgcn_raw_buffer_load_b128(r3, voff, rows[c] * a.pitch, kLoadAux);
+        x1 = __builtin_amdgcn_raw_buffer_load_b128(r3, voff, rows[c + 1] * a.pitch, kLoadAux);
+        x2 = __builtin_amdgcn_raw_buffer_load_b128(r3, voff, rows[c + 2] * a.pitch, kLoadAux);
+        asm volatile("" ::: "memory");  // issue here, not sunk into the uses
+    };
+    load3(0);
+    for (uint32_t t = 0; t < nt; ++t) {
+        uint32_t sel[4][8];
+        tri_sel(x0, x1, x2, sel);
+        load3(3 * t + 3);
+        tri_rows(sel, t);
     }
+    const uint32_t c = nt * 3;
+    if (c + 2 <= a.K) {
+        const u32x4 y0 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux);
+        const u32x4 y1 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c + 1] * a.pitch, kLoadAux);
+        mac_pair(y0, y1, c);
+    } else if (c < a.K) {
+        mac_input(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux), c);
     }
     bool mismatch = false;
 #pragma unroll
@@ -227,6 +259,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     if (mismatch) a.bad[obj] = 1u;  // same value from every writer: no atomic needed
     if (a.clear && v == 0) a.bad[obj] = 0u;
 }
+
+inline unsigned generic_lds(int K, int R) { return (unsigned)((K * R + 1) / 2 * 16 + K / 3 * R * 32); }
 
 // ----------------------------------------------------------------- launchers
 
@@ -498,16 +532,38 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     // upload the [K][R][kTabWords] table image and row indices once per plan
     hipError_t e = hipSuccess;
     std::call_once(p.dev_once, [&] {
-        // rows padded by 3 groups: the pipelined loop's loads reach up to two
-        // groups past the last input (through a zero-record resource)
-        std::vector<uint32_t> t((size_t)K * p.R * kTabWords), rows(K + 3 * kGroup, 0);
+        // rows padded: the pipelined loads reach up to 3 rows past the last
+        // triple (through a zero-record resource)
+        std::vector<uint32_t> t((size_t)K * p.R * kTabWords), rows(K + kRowPad, 0);
         for (int c = 0; c < K; ++c) {
             rows[c] = (uint32_t)p.in_rows[c];
             for (int r = 0; r < p.R; ++r)
                 for (int g = 0; g < kTabWords; ++g)
                     t[((size_t)c * p.R + r) * kTabWords + g] = p.tab[((size_t)r * K + c) * kTabWords + g];
         }
+        // input-triple tables [K/3][R][16]: words 0-7 the low halves (entries
+        // 0-3) of the eight 8-entry tables, words 8-15 their high halves
+        const GF &gf_ = gf();
+        const int nt = K / 3;
+        std::vector<uint32_t> t3((size_t)std::max(1, nt) * p.R * 16, 0);
+        for (int tr = 0; tr < nt; ++tr)
+            for (int r = 0; r < p.R; ++r) {
+                const uint8_t ca = p.coef[(size_t)r * K + 3 * tr], cb = p.coef[(size_t)r * K + 3 * tr + 1],
+                              cc = p.coef[(size_t)r * K + 3 * tr + 2];
+                uint32_t *w = &t3[((size_t)tr * p.R + r) * 16];
+                for (int j = 0; j < 8; ++j) {
+                    const uint8_t ent[8] = {
+                        gf_.mul(ca, (uint8_t)j), gf_.mul(ca, (uint8_t)(j << 3)),
+                        gf_.mul(cb, (uint8_t)j), gf_.mul(cb, (uint8_t)(j << 3)),
+                        gf_.mul(cc, (uint8_t)j), gf_.mul(cc, (uint8_t)(j << 3)),
+                        (uint8_t)(gf_.mul(ca, (uint8_t)((j >> 1) << 6)) ^ gf_.mul(cb, (uint8_t)((j & 1) << 7))),
+                        (uint8_t)(gf_.mul(cb, (uint8_t)((j & 1) << 6)) ^ gf_.mul(cc, (uint8_t)((j >> 1) << 6)))};
+                    for (int g = 0; g < 8; ++g) w[g + (j >> 2) * 8] |= (uint32_t)ent[g] << (8 * (j & 3));
+                }
+            }
         e = hipMalloc(&p.d_tab, t.size() * 4);
+        if (e == hipSuccess) e = hipMalloc(&p.d_tab3, t3.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(p.d_tab3, t3.data(), t3.size() * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMalloc(&p.d_in_row, rows.size() * 4);
         if (e == hipSuccess) e = hipMemcpy(p.d_tab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(p.d_in_row, rows.data(), rows.size() * 4, hipMemcpyHostToDevice);
@@ -522,6 +578,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     a.K = (uint32_t)K;
     a.rstride = (uint32_t)p.R;
     a.tab = p.d_tab + (size_t)s.r0 * kTabWords;
+    a.tab3 = p.d_tab3 + (size_t)s.r0 * 16;
     a.in_row = p.d_in_row;
     a.pitch = (uint32_t)L.pitch;
     a.packed = tail_part(row_space(L), a.nvec);
@@ -542,13 +599,9 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
         unsigned grid;
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
-        // full occupancy: the wide generic passes are VALU-bound (tools/kbench
-        // lib:SHAPE with caps of 2/4/6 workgroups per CU: -8/-1/+0.8 points)
-        // pipelined input groups for R <= 4 (tools/kbench lib:SHAPE, cold:
-        // RS(20+4) encode 65.9 -> 68.0 %, decode 64.8 -> 66.1 %; R = 8 shapes
-        // lost 2-3 points to the extra VGPRs, so they keep one group at a time)
-        hipLaunchKernelGGL((gf_apply_generic<R, kGroup, (R <= 4)>), dim3(grid), dim3(kBlock), (unsigned)(K * R * 8),
-                           st, a);
+        // full occupancy: the wide generic passes are VALU-bound (caps of 2-6
+        // workgroups per CU lose 0.4-9 points, r02_kbench_generic_caps_pipelined.txt)
+        hipLaunchKernelGGL(gf_apply_generic<R>, dim3(grid), dim3(kBlock), generic_lds(K, R), st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
