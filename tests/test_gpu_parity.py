@@ -118,6 +118,31 @@ def test_encode_zero_and_ff(gpu):
         assert np.array_equal(sh[10], want[10]) and np.array_equal(sh[11], want[11])
 
 
+@pytest.mark.parametrize("k", [18, 19, 20, 21, 22, 23])
+def test_generic_triples_every_remainder(gpu, k):
+    """The generic kernel codes inputs three at a time and the K mod 3
+    leftover as a pair or one input (gf_kernels.hip gf_apply_generic): every
+    remainder, every pass width R = 1..8 (and 9 = 8 + 1), against the oracle,
+    with rows of several workgroup chunks and a ragged last vector."""
+    size = 4100
+    for p in (1, 2, 3, 5, 7, 8, 9):
+        want = _full(k, p, size, idx=k * 31 + p)
+        enc = ia.New(k, p)
+        sh = [want[i].copy() for i in range(k)] + [np.zeros(size, np.uint8) for _ in range(p)]
+        enc.Encode(sh)
+        for r in range(k, k + p):
+            assert np.array_equal(sh[r], want[r]), (k, p, r)
+        assert enc.Verify(sh), (k, p)  # K = k + p inputs, all check rows
+        sh[k - 1][size - 1] ^= 0x5A
+        assert not enc.Verify(sh), (k, p)
+        sh[k - 1][size - 1] ^= 0x5A
+        lost = [0, k - 1] if p >= 2 else [k // 2]
+        part = [None if i in lost else sh[i].copy() for i in range(k + p)]
+        enc.ReconstructData(part)
+        for i in lost:
+            assert np.array_equal(part[i], want[i]), (k, p, i)
+
+
 @pytest.mark.parametrize("k,p,kind", [(1, 1, "vandermonde"), (3, 13, "vandermonde"),
                                       (4, 2, "cauchy"), (6, 3, "par1"), (10, 6, "vandermonde"),
                                       (16, 4, "vandermonde"), (17, 3, "vandermonde"),
