@@ -189,6 +189,17 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
                                  max_goroutines=32)
         sreps += 1
     split_val = ns * sreps * w["nbytes"] * len(w["ops"]) / (time.perf_counter() - t1) / GiB
+    # the host's one-thread memory rate beside it: the 1-core coder figure
+    # follows it from box to box (r02 runs: 17-36 GiB/s on the same code)
+    src = np.ones(1 << 28, np.uint8)
+    dst = np.empty_like(src)
+    np.copyto(dst, src)
+    creps, t2 = 0, time.perf_counter()
+    while time.perf_counter() - t2 < 0.5:
+        np.copyto(dst, src)
+        creps += 1
+    copy_gbps = 2 * src.nbytes * creps / (time.perf_counter() - t2) / 1e9
+    del src, dst
     L = oracle.lib()
     L.orc_cpu_isa.restype = ctypes.c_char_p
     isa = L.orc_cpu_isa().decode()
@@ -206,6 +217,7 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
         "windows_GiBps": [round(v, 2) for v in all_w],
         "one_core": {"value": round(one_v, 3), "cores": 1, "windows_GiBps": [round(v, 2) for v in one_w]},
         "per_object_split_form_GiBps": round(split_val, 3),
+        "host_copy_GBps_1thread": round(copy_gbps, 1),
         "sample": f"{ns} x {w['nbytes'] >> 10} KiB objects ({' + '.join(w['ops'])}), object-parallel; value = "
                   f"median of {windows} windows on {threads} threads (the box's cgroup share), one_core = "
                   f"median of {windows} windows on 1 thread, same sample; {isa} coder "
