@@ -100,6 +100,12 @@ WORKLOADS = {
     # a healthy RS(10+4) Get receives exactly k = 10 bodies (proxy first-d
     # rule): data {0,5} and parity {12,13} absent; ReconstructData rebuilds
     # the 2 data shards from the 10 survivors
+    # a wide code (K > 16: the generic kernel, inputs coded in triples);
+    # the Get receives k = 20 bodies, data {0,5} and parity {22,23} absent
+    "wide": dict(k=20, p=4, nbytes=1 << 20, batch=1024, lost=(0, 5), absent=(22, 23),
+                 ops=("encode", "decode"),
+                 desc="RS(20+4) encode+decode, 1 MiB objects, batch 1024/GPU, device-resident "
+                      "(generic kernel)"),
     "dec4": dict(k=10, p=4, nbytes=4 << 20, batch=512, lost=(0, 5), absent=(12, 13),
                  ops=("decode",), data_only=True,
                  desc="RS(10+4) ReconstructData, data shards {0,5} missing (10 of 14 present), "
@@ -111,6 +117,7 @@ METRICS = {
     "enc": "RS(10+2) encode GiB/s (device-resident), 1 MB objects",
     "encdec_upstream": "RS(10+2) encode+decode GiB/s (device-resident, unfused Reconstruct+Verify Get), 1 MB objects",
     "small": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
+    "wide": "RS(20+4) encode+decode GiB/s (device-resident), 1 MB objects",
     "small_mixed": "RS(10+2) encode+decode GiB/s (device-resident, mixed erasure patterns), 4 KiB objects",
     "small1k": "RS(10+2) encode+decode GiB/s (device-resident), 1 KiB objects",
     "small1k_sm": "RS(10+2) encode+decode GiB/s (device-resident, shard-major batch), 1 KiB objects",
@@ -512,7 +519,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps (default 3; 300 for the VALU-bound wide workload, whose "
+                         "shader clock ramps over the first ~0.1 s of load)")
     ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace", "latency"])
     ap.add_argument("--trace-objects", type=int, default=512)
     ap.add_argument("--devices", type=int, default=1,
@@ -527,6 +536,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     args = ap.parse_args()
+    if args.warmup is None:
+        # the HBM-bound workloads time the same with 3 or 1000 warmup steps;
+        # the VALU-bound wide code reads ~10 % slow until the clock has ramped
+        # (profiles/r02_bench_warmup.txt)
+        args.warmup = 300 if WORKLOADS.get(args.workload, {}).get("k", 0) > 16 else 3
 
     if args.workload == "trace":
         return run_trace(args)
@@ -689,7 +703,9 @@ def main():
 
     # algorithmic bytes per launch: encode k*S read + p*S write;
     # decode (e missing data rows) k*S read + e*S write; on unpadded S
-    e_rows = len(w["lost"])
+    # a Get's decode rebuilds every missing row, parity included (upstream
+    # Reconstruct, ecRedis.go:415), unless the workload is ReconstructData
+    e_rows = len(w["lost"]) + (0 if w.get("data_only") else len(w.get("absent", ())))
     enc_bytes = nobj * (k + p) * S
     dec_bytes = nobj * (k + e_rows) * S
     if w.get("upstream_get"):  # + Verify: reads all k+p rows again
@@ -700,6 +716,8 @@ def main():
     # rocprofv3 --stats reports it
     enc_sym = f"gf_apply_kernel<{k},{p}>"
     dec_sym = f"gf_apply_kernel<{k},{e_rows}>"
+    if k > 16:  # generic kernel, one launch per <= 8 rows
+        enc_sym, dec_sym = f"gf_apply_generic<{min(p, 8)}>", f"gf_apply_generic<{e_rows}>"
     if w.get("mixed"):  # device-resolved patterns: KMAX = n inputs (gf_masked.h)
         dec_sym = f"gf_apply_{'lanes' if ((S + 15) // 16) * 2 <= 256 else 'masked'}<{n},{min(p, 4)}>"
     if w.get("upstream_get"):
