@@ -520,8 +520,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=None,
-                    help="untimed steps (default 3; 300 for the VALU-bound wide workload, whose "
-                         "shader clock ramps over the first ~0.1 s of load)")
+                    help="untimed steps (default 300 for the device-resident workloads: the shader "
+                         "clock ramps over the first ~0.1 s of load; 3 for trace/latency)")
     ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace", "latency"])
     ap.add_argument("--trace-objects", type=int, default=512)
     ap.add_argument("--devices", type=int, default=1,
@@ -537,10 +537,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     args = ap.parse_args()
     if args.warmup is None:
-        # the HBM-bound workloads time the same with 3 or 1000 warmup steps;
-        # the VALU-bound wide code reads ~10 % slow until the clock has ramped
-        # (profiles/r02_bench_warmup.txt)
-        args.warmup = 300 if WORKLOADS.get(args.workload, {}).get("k", 0) > 16 else 3
+        # ~0.1-0.2 s of untimed steps: the HBM-bound workloads time the same
+        # with 3 or 1000 (the headline: 4,530-4,555 GiB/s), but the VALU-
+        # heavier passes read slow until the shader clock has ramped (wide
+        # RS(20+4) -10 %, 4 KiB mixed patterns -6 %; profiles/r02_bench_warmup*.txt)
+        args.warmup = 3 if args.workload in ("trace", "latency") else 300
 
     if args.workload == "trace":
         return run_trace(args)
