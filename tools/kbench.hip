@@ -1248,7 +1248,10 @@ int lib_time(std::string spec, int rounds) {
     if (op == "enc") plan = ctx->plan_encode();
     else if (op == "ver") plan = ctx->plan_verify();
     else {
-        present[0] = present[1] = 0;
+        // KB_LOST="a,b": the lost data rows (default 0,1)
+        int l0 = 0, l1 = 1;
+        if (const char *e = std::getenv("KB_LOST")) std::sscanf(e, "%d,%d", &l0, &l1);
+        present[l0] = present[l1] = 0;
         ctx->plan_reconstruct(present.data(), false, true, plan);
     }
     const size_t nbytes = (size_t)(obj_mib * (1 << 20)), S = (nbytes + k - 1) / k;
