@@ -117,9 +117,32 @@ struct GenericArgs {
     uint32_t out_off[kMaxRG];
 };
 
+// 8-B vector store of the generic kernel's VW = 2 form; `part` (0..7) as in
+// store_row: only the row's first `part` bytes of the last vector
+template <int SAUX>
+__device__ __forceinline__ void store_row8(const u32x2 &o, __amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
+                                           uint32_t part) {
+    if (part == 0u) {
+        __builtin_amdgcn_raw_buffer_store_b64(o, rs, voff, soff, SAUX);
+        return;
+    }
+    uint32_t off = 0, rem = o[0];
+    if (part & 4u) {
+        __builtin_amdgcn_raw_buffer_store_b32(o[0], rs, voff, soff, SAUX);
+        off = 4;
+        rem = o[1];
+    }
+    if (part & 2u) {
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)rem, rs, voff + off, soff, SAUX);
+        off += 2;
+        rem >>= 16;
+    }
+    if (part & 1u) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)rem, rs, voff + off, soff, SAUX);
+}
+
 // LDS: [K][R] u32x2 single-input table words 1 and 3, then [K/3][R][8] high
 // words of the triple tables (generic_lds)
-template <int R>
+template <int R, int VW>
 __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
@@ -145,26 +168,32 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     // loads past the last triple go through a zero-record resource: no memory
     // traffic, and the wait counts stay static
     const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, 0, 0x00020000);
-    const uint32_t voff = v * 16u;
+    const uint32_t voff = v * (4u * VW);
+    // one lane's vector of VW dwords (VW = 2: the upper half stays zero, unused)
+    auto ldv = [](__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so, int) -> u32x4 {
+        if (VW == 4) return __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, kLoadAux);
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, kLoadAux);
+        return u32x4{t[0], t[1], 0u, 0u};
+    };
     const constant_ptr<uint32_t> tab = (constant_ptr<uint32_t>)a.tab;
     const constant_ptr<uint32_t> rows = (constant_ptr<uint32_t>)a.in_row;
-    uint32_t acc[R][4];
+    uint32_t acc[R][VW];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+        for (int d = 0; d < VW; ++d) acc[r][d] = 0;
     // keep the input-at-a-time order: without these fences the scheduler
     // hoists every input's index math and splits the work row by row
     auto fence = [&] {
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+            for (int d = 0; d < VW; ++d) asm volatile("" : "+v"(acc[r][d]));
     };
     auto mac_input = [&](const u32x4 &x, uint32_t c) {
         const constant_ptr<uint32_t> t = tab + (size_t)c * a.rstride * kTabWords;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
+        for (int d = 0; d < VW; ++d) {
             const GfIdx g = gf_idx(x[d]);
 #pragma unroll
             for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], t + r * kTabWords, g);
@@ -175,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
         const constant_ptr<uint32_t> ta = tab + (size_t)c * a.rstride * kTabWords;
         const constant_ptr<uint32_t> tb = ta + (size_t)a.rstride * kTabWords;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
+        for (int d = 0; d < VW; ++d) {
             const GfIdx ga = gf_idx(xa[d]), gb = gf_idx(xb[d]);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -191,7 +220,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     // selectors of one triple (the 8 groups above) for the lane's 4 dwords
     auto tri_sel = [&](const u32x4 &xa, const u32x4 &xb, const u32x4 &xc, uint32_t (&sel)[4][8]) {
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
+        for (int d = 0; d < VW; ++d) {
             sel[d][0] = xa[d] & 0x07070707u;
             sel[d][1] = (xa[d] >> 3) & 0x07070707u;
             sel[d][2] = xb[d] & 0x07070707u;
@@ -211,7 +240,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
             const constant_ptr<uint32_t> L = T + r * 16;
             const u32x4 h0 = lv3[(t * R + r) * 2], h1 = lv3[(t * R + r) * 2 + 1];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
+            for (int d = 0; d < VW; ++d) {
                 uint32_t q = xor3(acc[r][d], lut8(L[0], h0[0], sel[d][0]), lut8(L[1], h0[1], sel[d][1]));
                 q = xor3(q, lut8(L[2], h0[2], sel[d][2]), lut8(L[3], h0[3], sel[d][3]));
                 q = xor3(q, lut8(L[4], h1[0], sel[d][4]), lut8(L[5], h1[1], sel[d][5]));
@@ -224,9 +253,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     u32x4 x0, x1, x2;
     auto load3 = [&](uint32_t c) {
         const __amdgpu_buffer_rsrc_t r3 = c < nt * 3 ? rs : rsn;
-        x0 = __builtin_amdgcn_raw_buffer_load_b128(r3, voff, rows[c] * a.pitch, kLoadAux);
-        x1 = __builtin_amdgcn_raw_buffer_load_b128(r3, voff, rows[c + 1] * a.pitch, kLoadAux);
-        x2 = __builtin_amdgcn_raw_buffer_load_b128(r3, voff, rows[c + 2] * a.pitch, kLoadAux);
+        x0 = ldv(r3, voff, rows[c] * a.pitch, kLoadAux);
+        x1 = ldv(r3, voff, rows[c + 1] * a.pitch, kLoadAux);
+        x2 = ldv(r3, voff, rows[c + 2] * a.pitch, kLoadAux);
         asm volatile("" ::: "memory");  // issue here, not sunk into the uses
     };
     load3(0);
@@ -238,22 +267,27 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
     }
     const uint32_t c = nt * 3;
     if (c + 2 <= a.K) {
-        const u32x4 y0 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux);
-        const u32x4 y1 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c + 1] * a.pitch, kLoadAux);
+        const u32x4 y0 = ldv(rs, voff, rows[c] * a.pitch, kLoadAux);
+        const u32x4 y1 = ldv(rs, voff, rows[c + 1] * a.pitch, kLoadAux);
         mac_pair(y0, y1, c);
     } else if (c < a.K) {
-        mac_input(__builtin_amdgcn_raw_buffer_load_b128(rs, voff, rows[c] * a.pitch, kLoadAux), c);
+        mac_input(ldv(rs, voff, rows[c] * a.pitch, kLoadAux), c);
     }
     bool mismatch = false;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if ((uint32_t)r < a.nw) {
-            u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-            store_row<kStoreAux>(o, rs, voff, a.out_off[r], v == a.nvec - 1 ? a.packed : 0u);
+            if (VW == 4) {
+                u32x4 o = {acc[r][0], acc[r][1], acc[r][VW > 2 ? 2 : 0], acc[r][VW > 3 ? 3 : 0]};
+                store_row<kStoreAux>(o, rs, voff, a.out_off[r], v == a.nvec - 1 ? a.packed : 0u);
+            } else {
+                store_row8<kStoreAux>(u32x2{acc[r][0], acc[r][1]}, rs, voff, a.out_off[r],
+                                      v == a.nvec - 1 ? a.packed : 0u);
+            }
         } else {
-            const uint32_t valid = (v == a.nvec - 1) ? a.tail : 16u;
+            const uint32_t valid = (v == a.nvec - 1) ? a.tail : 4u * VW;
 #pragma unroll
-            for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+            for (int d = 0; d < VW; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
         }
     }
     if (mismatch) a.bad[obj] = 1u;  // same value from every writer: no atomic needed
@@ -570,10 +604,17 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         p.dev_err = e;
     });
     if (p.dev_err != hipSuccess) return p.dev_err;
+    // 8-B lane vectors for narrow passes that write rows: 51 VGPRs at R = 4
+    // (8 waves) against 81 (5 waves); RS(20+4) encode +2.5, RS(17+3) +3
+    // points, the wide encode+decode workload +3 %.  Wider passes and
+    // check-only passes keep 16 B (R = 8: -1 to -3 points; Verify -1.4)
+    // (profiles/r02_kbench_generic_vw2*.txt)
+    const int vw = (R <= 4 && s.nw > 0) ? 2 : 4;
+    const uint32_t vb = vw == 2 ? 8u : 16u;  // bytes per lane vector
     GenericArgs a;
     a.obj_stride = L.obj_stride;
-    a.nvec = (uint32_t)((L.shard_len + 15) / 16);
-    a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
+    a.nvec = (uint32_t)((L.shard_len + vb - 1) / vb);
+    a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * vb);
     a.nw = (uint32_t)s.nw;
     a.K = (uint32_t)K;
     a.rstride = (uint32_t)p.R;
@@ -581,7 +622,10 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     a.tab3 = p.d_tab3 + (size_t)s.r0 * 16;
     a.in_row = p.d_in_row;
     a.pitch = (uint32_t)L.pitch;
-    a.packed = tail_part(row_space(L), a.nvec);
+    {
+        const size_t w = row_space(L) - (size_t)(a.nvec - 1) * vb;
+        a.packed = w < vb ? (uint32_t)w : 0u;
+    }
     int maxrow = 0;
     for (int c = 0; c < K; ++c) maxrow = std::max(maxrow, p.in_rows[c]);
     for (int r = 0; r < R; ++r) {
@@ -589,7 +633,7 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * L.pitch);
         maxrow = std::max(maxrow, row);
     }
-    a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * 16);
+    a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * vb);
     const unsigned gx = (a.nvec + kBlock - 1) / kBlock;
     const int step = max_items(gx);
     for (int o0 = 0; o0 < L.nobj; o0 += step) {
@@ -601,7 +645,10 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
         // full occupancy: the wide generic passes are VALU-bound (caps of 2-6
         // workgroups per CU lose 0.4-9 points, r02_kbench_generic_caps_pipelined.txt)
-        hipLaunchKernelGGL(gf_apply_generic<R>, dim3(grid), dim3(kBlock), generic_lds(K, R), st, a);
+        if (vw == 2)
+            hipLaunchKernelGGL((gf_apply_generic<R, 2>), dim3(grid), dim3(kBlock), generic_lds(K, R), st, a);
+        else
+            hipLaunchKernelGGL((gf_apply_generic<R, 4>), dim3(grid), dim3(kBlock), generic_lds(K, R), st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
