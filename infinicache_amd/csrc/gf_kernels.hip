@@ -102,7 +102,10 @@ Plan::~Plan() {
 //     operand of each lookup its SGPR, the other must be a VGPR) are staged
 //     in LDS once per workgroup and read as broadcast ds_read_b128;
 //   * K mod 3 leftover inputs go as a pair (6 lookups, 3 xor3) or one input
-//     through the 5-word single-coefficient tables.
+//     through the 5-word single-coefficient tables;
+//   * passes of <= 4 written rows use 8-B lane vectors (VW = 2: half the
+//     accumulator and selector registers, 8 waves per SIMD), wider and
+//     check-only passes 16 B (launch_generic).
 constexpr int kMaxRG = 8;
 constexpr int kRowPad = 8;  // row-index image padding past K (the pipelined loads' over-reach)
 struct GenericArgs {
