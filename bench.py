@@ -184,6 +184,14 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
     all_v, all_w = rate(threads, ns, budget_s * 0.5 / windows)
     one_v, one_w = rate(1, ns, budget_s * 0.3 / windows)  # same sample: beyond the host's L3
     exact = bool(np.array_equal(sample[:, :, :S], gpu_sample[:, :, :S]))
+    if "encode" in w["ops"] and "decode" in w["ops"]:
+        # the encode pass above needs the data rows, so the rows the GPU
+        # rebuilt are checked by a separate CPU decode: erase them again and
+        # rebuild them on the CPU from the GPU's survivors
+        dsample = gpu_sample.copy()
+        dsample[:, lost] = 0
+        oracle.code_batch(inv_rows, surv, lost, dsample.reshape(-1), n * pitch, pitch, S, ns, nthreads=threads)
+        exact = exact and bool(np.array_equal(dsample[:, :, :S], gpu_sample[:, :, :S]))
     # per-object codeSomeShardsP form, ~budget/5 s
     sreps, t1 = 0, time.perf_counter()
     while time.perf_counter() - t1 < budget_s / 5:
@@ -230,7 +238,8 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
                   f"median of {windows} windows on 1 thread, same sample; {isa} coder "
                   f"(oracle/rs_oracle.c restating upstream's SIMD path; Go toolchain and "
                   f"klauspost/reedsolomon unavailable offline); per-object codeSomeShardsP split "
-                  f"form {split_val:.2f} GiB/s; host CPU: {cpu_model}; bit-exact vs GPU: {exact}",
+                  f"form {split_val:.2f} GiB/s; host CPU: {cpu_model}; bit-exact vs GPU (parity, and the rows "
+                  f"the GPU rebuilt from garbage in the work check): {exact}",
     }
 
 
@@ -646,6 +655,56 @@ def main():
             enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, stream)
 
     op_fns = {"encode": op_encode, "decode": op_decode}
+
+    # rows each op writes, per (object, shard row)
+    written = {}
+    if "encode" in w["ops"]:
+        e_enc = torch.zeros((nobj, n), dtype=torch.bool, device=dev)
+        e_enc[:, k:] = True
+        written["encode"] = e_enc
+    if "decode" in w["ops"]:
+        if w.get("mixed"):
+            e_dec = torch.from_numpy(pres_m == 0).to(dev)
+        else:
+            rows = list(w["lost"]) + ([] if w.get("data_only") else list(w.get("absent", ())))
+            e_dec = torch.zeros((nobj, n), dtype=torch.bool, device=dev)
+            e_dec[:, rows] = True
+        written["decode"] = e_dec
+
+    def check_ops(buf):
+        """Garbage into every row the op writes, the op, then a bit-exact
+        compare of those rows' shard_len bytes with the copy taken before."""
+        out = {}
+        gg = torch.Generator(device=dev).manual_seed(0xBAD + rank)
+        for op in w["ops"]:
+            ref = buf.clone()
+            E = written[op]
+            if w.get("shard_major"):
+                pieces = buf[:, :nobj * stride].view(n, nobj, stride)
+                Et = E.t().contiguous()
+                pieces[Et] = torch.randint(0, 256, (int(Et.sum()), stride), dtype=torch.uint8, device=dev,
+                                           generator=gg)
+            else:
+                buf[E] = torch.randint(0, 256, (int(E.sum()), pitch), dtype=torch.uint8, device=dev, generator=gg)
+            flags = op == "decode" and not w.get("data_only")  # the decode sets every object's flag
+            if flags:
+                bad.fill_(7)
+            op_fns[op](buf)
+            torch.cuda.synchronize(dev)
+            if flags and int(bad.sum()) != 0:
+                raise SystemExit(f"{op} check: decode reported a mismatch / error status")
+            if w.get("shard_major"):
+                same = torch.equal(buf[:, :nobj * stride].view(n, nobj, stride)[..., :S],
+                                   ref[:, :nobj * stride].view(n, nobj, stride)[..., :S])
+            else:
+                same = torch.equal(buf[..., :S], ref[..., :S])
+            del ref
+            if not same:
+                raise SystemExit(f"{op} check FAILED: rewritten rows differ from the rows before")
+            out[op] = {"result": "bit-exact", "objects": nobj, "rows_rewritten": int(E.sum()),
+                       "bytes_compared": int(E.sum()) * S}
+        return out
+
     turn = [0]
 
     def step(fixed=None):
@@ -677,6 +736,11 @@ def main():
     objs_all = dctx.sum(nobj)
     if int(bad.sum()) != 0:
         raise SystemExit("decode reported a verify mismatch on synthetic data")
+    # Untimed proof that the timed ops did their work: on batch 0, overwrite
+    # every row an op writes (encode: the parity rows; decode: each object's
+    # erased rows) with random garbage, run the op, and compare the rows'
+    # shard_len bytes with a copy taken before (client/ecRedis.go:390,404-427).
+    work_check = check_ops(bufs[0])
     kms_alone = kernel_ms()
     # Each op's share of the timed step comes from its uninterrupted run; run
     # alone an op can be a little slower than inside the step (there a decode
@@ -769,7 +833,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and not w.get("shard_major"):
         from oracle import rs_numpy as rn
         ns = min(256, nobj)  # 256 x 1.26 MB: well beyond the host's last-level cache
-        gpu_sample = bufs[0][:ns].cpu().numpy()  # final GPU state of the sampled objects
+        # final GPU state of the sampled objects: batch 0 after check_ops, so
+        # its parity rows and erased rows are the ones the GPU rewrote from garbage
+        gpu_sample = bufs[0][:ns].cpu().numpy()
         sample = gpu_sample.copy()
         if "encode" in w["ops"]:
             sample[:, k:] = 0           # CPU recomputes parity from the same data rows
@@ -807,9 +873,15 @@ def main():
                 "batch_per_gpu": nobj,
                 "batch_copies": copies,
                 "decode_erasures": list(w["lost"]),
-                "parallelism": f"object-per-rank x{world} (RCCL all_reduce barrier only)",
+                "parallelism": (f"object-per-rank x{world} "
+                                + ("(one process, no collective)" if world == 1 else
+                                   f"({'RCCL' if backend == 'nccl' else backend} all_reduce barrier only"
+                                   + (", ranks sharing one GPU)" if os.environ.get("BENCH_SHARE_GPU") == "1"
+                                      else ")"))),
             },
             "roofline": roofline,
+            **({"decode_check": work_check["decode"]["result"]} if "decode" in work_check else {}),
+            "work_check": work_check,
             **({"warm_repeat": warm} if warm else {}),
             "cpu_baseline": cpu,
         }

@@ -78,12 +78,20 @@ void rsgpu_destroy(rsgpu_ctx *ctx);
  * An object's shards never leave one GPU: per-object host calls go to the
  * devices round-robin, batch host calls send object o to devices[o % ndev]
  * and run the devices' pipelines in parallel (one PCIe link each),
- * device-resident calls run on the device that owns d_base.  Duplicate
- * devices: RSGPU_ERR_INVALID_ARG. */
+ * device-resident calls run on the device that owns d_base.  A device may be
+ * listed more than once: every entry is an independent single-device context
+ * (its own streams, staging slots and batch pipeline, e.g. two pipelines
+ * feeding one GPU), and device-resident calls on memory of a device listed
+ * several times go to its entries in turn. */
 int rsgpu_create_multi(int data_shards, int parity_shards, const int *devices, int ndev, unsigned flags,
                        rsgpu_ctx **out);
-/* The context's devices (up to cap written to out); returns their number. */
+/* The context's devices, one per entry of its device list (up to cap written
+ * to out); returns their number. */
 int rsgpu_devices(const rsgpu_ctx *ctx, int *out, int cap);
+/* Per entry of rsgpu_devices: the number of compute calls that entry has run
+ * on its device so far (batch calls count once per entry they reached).
+ * Returns the number of entries.  Lets a caller see how its work spread. */
+int rsgpu_device_calls(const rsgpu_ctx *ctx, uint64_t *out, int cap);
 
 int rsgpu_data_shards(const rsgpu_ctx *ctx);
 int rsgpu_parity_shards(const rsgpu_ctx *ctx);

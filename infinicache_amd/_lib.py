@@ -24,7 +24,7 @@ EXPORTS = (
     "rsgpu_host_register", "rsgpu_host_unregister", "rsgpu_host_alloc", "rsgpu_host_free",
     "rsgpu_encode_verify", "rsgpu_decode_dev_masks", "rsgpu_reconstruct_dev_masks",
     "rsgpu_create_multi", "rsgpu_devices", "rsgpu_encode_image", "rsgpu_encode_verify_image",
-    "rsgpu_verify_image", "rsgpu_reconstruct_image", "rsgpu_decode_image",
+    "rsgpu_verify_image", "rsgpu_reconstruct_image", "rsgpu_decode_image", "rsgpu_device_calls",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -65,6 +65,7 @@ def load():
     L.rsgpu_create.argtypes = [ci, ci, ci, ctypes.c_uint, ctypes.POINTER(vp)]
     L.rsgpu_create_multi.argtypes = [ci, ci, intp, ci, ctypes.c_uint, ctypes.POINTER(vp)]
     L.rsgpu_devices.argtypes = [vp, intp, ci]
+    L.rsgpu_device_calls.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ci]
     L.rsgpu_destroy.argtypes = [vp]
     L.rsgpu_destroy.restype = None
     L.rsgpu_data_shards.argtypes = [vp]

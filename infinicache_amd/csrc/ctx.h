@@ -94,23 +94,37 @@ struct Pipeline {
 };
 
 // Device atlas of every erasure pattern of one operation (gf_masked.h),
-// built and uploaded on the first *_dev_masks call, then immutable.
+// built and uploaded on the first *_dev_masks call, then immutable.  The
+// host part is built once per code: a multi-device context's per-GPU
+// sub-contexts share their parent's (rsgpu_ctx::atlas_host); each uploads
+// its own device copy.  A failed upload (e.g. HBM momentarily exhausted)
+// frees what it allocated and is retried by the next call.
 struct Atlas {
-    std::once_flag host_once, dev_once;  // host build (no device needed), then upload
-    int host_err = 0, dev_err = 0;
+    std::once_flag host_once;  // host build (no device needed)
+    int host_err = 0;
+    std::mutex dev_mu;         // guards the upload below
+    bool dev_done = false;
     int32_t *d_pat = nullptr;
     void *d_recs = nullptr;
     uint32_t *d_tabs = nullptr;
     std::vector<int32_t> h_pat;   // pattern table, kept (host-flag calls validate with it)
-    std::vector<uint8_t> h_recs;  // PatRec image, freed after the upload
-    std::vector<uint32_t> h_tabs; // kernel tables, freed after the upload
+    std::vector<uint8_t> h_recs;  // PatRec image (freed after the upload unless shared)
+    std::vector<uint32_t> h_tabs; // kernel tables (freed after the upload unless shared)
     AtlasView view;
-    ~Atlas() {
+    void free_dev() {
         if (d_pat) (void)hipFree(d_pat);
         if (d_recs) (void)hipFree(d_recs);
         if (d_tabs) (void)hipFree(d_tabs);
+        d_pat = nullptr;
+        d_recs = nullptr;
+        d_tabs = nullptr;
     }
+    ~Atlas() { free_dev(); }
 };
+// Estimated bytes of an atlas's kernel tables (before building it): the
+// host-flag *_dev_multi calls take the atlas path only below a modest size
+// and keep the host-planned path for codes whose atlas would be large.
+size_t atlas_estimate(int k, int p, bool check);
 enum AtlasMode { kAtlasReconstruct = 0, kAtlasData = 1, kAtlasDecode = 2 };
 
 }  // namespace rsgpu
@@ -122,15 +136,18 @@ struct rsgpu_ctx {
     rsgpu::MultiWorkspace multi_ws;  // mixed-pattern device launches
     rsgpu::Atlas atlas[3];           // device-resolved patterns, per AtlasMode
     uint32_t *d_ctab = nullptr;      // [256][8] coefficient tables (gf_apply_lanes)
-    std::once_flag ctab_once;
-    int ctab_err = 0;
+    std::mutex ctab_mu;              // guards the d_ctab upload (retried after a failure)
     rsgpu::StatusScratch scratch;    // multi-reporter status of the masked decode
     // Multi-device context (rsgpu_create_multi / RSGPU_ALL_DEVICES): one
-    // single-device context per GPU.  Per-object calls go round-robin, batch
-    // calls split objects o -> device o mod N and run the devices in
-    // parallel, device-resident calls go to the device that owns the memory.
+    // single-device context per entry of the device list.  Per-object calls
+    // go round-robin, batch calls split objects o -> entry o mod N and run the
+    // entries in parallel, device-resident calls go to an entry that owns the
+    // memory (round-robin when a device is listed more than once: each entry
+    // has its own streams, staging slots and pipeline).
     std::vector<std::unique_ptr<rsgpu_ctx>> subs;
+    rsgpu_ctx *parent = nullptr;      // a sub-context's multi-device context (shared host atlas)
     std::atomic<unsigned> rr{0};
+    std::atomic<uint64_t> calls{0};   // compute calls that reached this (sub-)context's device
     bool multi() const { return !subs.empty(); }
     rsgpu_ctx *pick() { return subs[rr.fetch_add(1, std::memory_order_relaxed) % subs.size()].get(); }
     rsgpu_ctx *sub_for(const void *dev_ptr);  // rsgpu.cpp; nullptr: not memory of one of our devices
@@ -161,6 +178,7 @@ struct rsgpu_ctx {
             if (dev_state == 0) dev_state = rsgpu_device_ok(device) ? 1 : RSGPU_ERR_NO_DEVICE;
             if (dev_state < 0) return dev_state;
         }
+        calls.fetch_add(1, std::memory_order_relaxed);
         int cur = -1;
         HIP_TRY(hipGetDevice(&cur));
         if (cur != device) {

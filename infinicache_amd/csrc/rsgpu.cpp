@@ -298,9 +298,14 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
 // PatRec per (pattern, sub-pass) and its [kmax][R] kernel tables.  Built once
 // per context and mode (upstream's inversionTree holds the same inverses,
 // filled lazily), uploaded, then immutable.
+constexpr size_t kAtlasMaxBytes = (size_t)256 << 20;      // *_dev_masks: no other path
+constexpr size_t kAtlasHostFlagBytes = (size_t)32 << 20;  // *_dev_multi: host-planned path beyond
+
 int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
     const int n = ctx->n, k = ctx->k;
     const bool check = mode == kAtlasDecode, data_only = mode == kAtlasData;
+    // refuse before enumerating 2^n patterns whose tables could not be kept
+    if (atlas_estimate(k, ctx->p, check) > kAtlasMaxBytes) return RSGPU_ERR_NOT_IMPLEMENTED;
     const size_t nm = (size_t)1 << n;
     struct Ent {
         int K, R, nw, ki;
@@ -344,7 +349,7 @@ int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
     const int R = std::max(1, std::min(4, maxR)), nsub = std::max(1, (maxR + 3) / 4);
     const int kmax = check ? n : k;
     const size_t nrec = ents.size() * (size_t)nsub, tw = (size_t)kmax * R * kCoefWords;
-    if (nrec * tw * 4 > ((size_t)256 << 20)) return RSGPU_ERR_NOT_IMPLEMENTED;  // bound the atlas
+    if (nrec * tw * 4 > kAtlasMaxBytes) return RSGPU_ERR_NOT_IMPLEMENTED;  // bound the atlas
     std::vector<uint32_t> ct(256 * kCoefWords);
     for (int c = 0; c < 256; ++c) coef_tables((uint8_t)c, &ct[(size_t)c * kCoefWords]);
     std::vector<PatRec> recs(std::max<size_t>(nrec, 1));
@@ -393,19 +398,24 @@ int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
     return RSGPU_OK;
 }
 
-int upload_atlas(rsgpu_ctx *ctx, Atlas &A) {
-    HIP_TRY(hipMalloc(&A.d_pat, A.h_pat.size() * 4));
-    HIP_TRY(hipMemcpy(A.d_pat, A.h_pat.data(), A.h_pat.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&A.d_recs, A.h_recs.size()));
-    HIP_TRY(hipMemcpy(A.d_recs, A.h_recs.data(), A.h_recs.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&A.d_tabs, A.h_tabs.size() * 4));
-    HIP_TRY(hipMemcpy(A.d_tabs, A.h_tabs.data(), A.h_tabs.size() * 4, hipMemcpyHostToDevice));
-    std::vector<uint8_t>().swap(A.h_recs);
-    std::vector<uint32_t>().swap(A.h_tabs);
-    A.view.pat = A.d_pat;
-    A.view.recs = A.d_recs;
-    A.view.tabs = A.d_tabs;
-    A.view.ctab = ctx->d_ctab;
+// Uploads the host atlas H (this context's own, or its parent's when shared)
+// into D, this context's device copy.  On failure nothing stays allocated.
+int upload_atlas(rsgpu_ctx *ctx, const Atlas &H, Atlas &D) {
+    hipError_t e = hipMalloc(&D.d_pat, H.h_pat.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(D.d_pat, H.h_pat.data(), H.h_pat.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&D.d_recs, H.h_recs.size());
+    if (e == hipSuccess) e = hipMemcpy(D.d_recs, H.h_recs.data(), H.h_recs.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&D.d_tabs, H.h_tabs.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(D.d_tabs, H.h_tabs.data(), H.h_tabs.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        D.free_dev();
+        return hip_fail(e, "atlas upload");
+    }
+    D.view = H.view;
+    D.view.pat = D.d_pat;
+    D.view.recs = D.d_recs;
+    D.view.tabs = D.d_tabs;
+    D.view.ctab = ctx->d_ctab;
     return RSGPU_OK;
 }
 
@@ -432,15 +442,32 @@ int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_
 rsgpu_ctx *rsgpu_ctx::sub_for(const void *dev_ptr) {
     hipPointerAttribute_t at;
     if (!dev_ptr || hipPointerGetAttributes(&at, dev_ptr) != hipSuccess) return nullptr;
-    for (auto &c : subs)
-        if (c->device == at.device) return c.get();
+    // a device listed several times: its entries take turns
+    const unsigned start = rr.fetch_add(1, std::memory_order_relaxed);
+    for (size_t i = 0; i < subs.size(); ++i) {
+        rsgpu_ctx *c = subs[(start + i) % subs.size()].get();
+        if (c->device == at.device) return c;
+    }
     return nullptr;
+}
+
+size_t rsgpu::atlas_estimate(int k, int p, bool check) {
+    const int n = k + p;
+    double npat = 0, c = 1;  // sum over j >= k of C(n, j)
+    for (int j = 0; j <= n; ++j) {
+        if (j >= k) npat += c;
+        c = c * (n - j) / (j + 1);
+    }
+    const int R = std::min(4, p), nsub = (p + 3) / 4, kmax = check ? n : k;
+    const double b = npat * nsub * ((double)kmax * R * kCoefWords * 4 + sizeof(PatRec));
+    return b > 1e18 ? (size_t)-1 : (size_t)b;
 }
 
 int rsgpu_ctx::atlas_host(AtlasMode mode, const Atlas *&out) {
     if (n > kAtlasMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
-    Atlas &A = atlas[mode];
-    std::call_once(A.host_once, [&] { A.host_err = build_atlas_host(this, mode, A); });
+    rsgpu_ctx *owner = parent ? parent : this;  // one host build per code
+    Atlas &A = owner->atlas[mode];
+    std::call_once(A.host_once, [&] { A.host_err = build_atlas_host(owner, mode, A); });
     out = &A;
     return A.host_err;
 }
@@ -449,18 +476,34 @@ int rsgpu_ctx::atlas_view(AtlasMode mode, AtlasView &out) {
     const Atlas *ah;
     int e = atlas_host(mode, ah);
     if (e) return e;
-    std::call_once(ctab_once, [&] {
-        std::vector<uint32_t> t(256 * kCtabStride, 0);
-        for (int c = 0; c < 256; ++c) coef_tables((uint8_t)c, &t[(size_t)c * kCtabStride]);
-        hipError_t e = hipMalloc(&d_ctab, t.size() * 4);
-        if (e == hipSuccess) e = hipMemcpy(d_ctab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
-        ctab_err = e == hipSuccess ? RSGPU_OK : hip_fail(e, "atlas coefficient table");
-    });
-    if (ctab_err) return ctab_err;
-    Atlas &A = atlas[mode];
-    std::call_once(A.dev_once, [&] { A.dev_err = upload_atlas(this, A); });
-    if (A.dev_err) return A.dev_err;
-    out = A.view;
+    {
+        std::lock_guard<std::mutex> g(ctab_mu);
+        if (!d_ctab) {
+            std::vector<uint32_t> t(256 * kCtabStride, 0);
+            for (int c = 0; c < 256; ++c) coef_tables((uint8_t)c, &t[(size_t)c * kCtabStride]);
+            uint32_t *d = nullptr;
+            hipError_t he = hipMalloc(&d, t.size() * 4);
+            if (he == hipSuccess) he = hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+            if (he != hipSuccess) {
+                if (d) (void)hipFree(d);
+                return hip_fail(he, "atlas coefficient table");  // retried by the next call
+            }
+            d_ctab = d;
+        }
+    }
+    Atlas &D = atlas[mode];
+    std::lock_guard<std::mutex> g(D.dev_mu);
+    if (!D.dev_done) {
+        if ((e = upload_atlas(this, *ah, D))) return e;  // retried by the next call
+        D.dev_done = true;
+        // a context of its own (no sub-contexts share its host atlas) drops
+        // the host images once they are on the device
+        if (ah == &D && subs.empty() && !parent) {
+            std::vector<uint8_t>().swap(D.h_recs);
+            std::vector<uint32_t>().swap(D.h_tabs);
+        }
+    }
+    out = D.view;
     return RSGPU_OK;
 }
 
@@ -577,11 +620,12 @@ int rsgpu_create_multi(int data_shards, int parity_shards, const int *devices, i
     int e = rsgpu_create(data_shards, parity_shards, devices[0] < 0 ? -2 : devices[0], flags, &parent);
     if (e) return e;
     std::unique_ptr<rsgpu_ctx> P(parent);
+    // a device may be listed more than once: each entry is an independent
+    // single-device context (its own streams, staging slots and pipeline)
     for (int i = 0; i < ndev; ++i) {
-        for (int j = 0; j < i; ++j)
-            if (devices[j] == devices[i]) return RSGPU_ERR_INVALID_ARG;
         rsgpu_ctx *c = nullptr;
         if ((e = rsgpu_create(data_shards, parity_shards, devices[i] < 0 ? -2 : devices[i], flags, &c))) return e;
+        c->parent = P.get();
         P->subs.emplace_back(c);
     }
     *out = P.release();
@@ -595,6 +639,17 @@ int rsgpu_devices(const rsgpu_ctx *ctx, int *out, int cap) {
         return 1;
     }
     for (int i = 0; i < (int)ctx->subs.size() && i < cap; ++i) out[i] = ctx->subs[i]->device;
+    return (int)ctx->subs.size();
+}
+
+int rsgpu_device_calls(const rsgpu_ctx *ctx, uint64_t *out, int cap) {
+    if (!ctx || cap < 0 || (cap > 0 && !out)) return RSGPU_ERR_INVALID_ARG;
+    if (!ctx->multi()) {
+        if (cap > 0) out[0] = ctx->calls.load(std::memory_order_relaxed);
+        return 1;
+    }
+    for (int i = 0; i < (int)ctx->subs.size() && i < cap; ++i)
+        out[i] = ctx->subs[i]->calls.load(std::memory_order_relaxed);
     return (int)ctx->subs.size();
 }
 
@@ -1014,10 +1069,16 @@ static int recon_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
     if (e) return e;
     const int n = ctx->n;
     if (nobj == 0) return RSGPU_OK;
-    if (n <= kAtlasMaxN && !((uintptr_t)d_base & 15) && !(pitch & 15) && !(obj_stride & 15))
-        return recon_dev_multi_atlas(ctx, d_base, present, shard_len, pitch, obj_stride, nobj,
-                                     check ? kAtlasDecode : data_only ? kAtlasData : kAtlasReconstruct, d_bad,
-                                     stream);
+    // the device-resolved kernels for codes whose atlas is modest (RS(10+2):
+    // 30 KB; RS(12+4): ~1 MB); wider atlases (e.g. RS(4+12), RS(2+14)) keep the
+    // host-planned path below rather than building tens of thousands of
+    // patterns on the first call
+    if (n <= kAtlasMaxN && !((uintptr_t)d_base & 15) && !(pitch & 15) && !(obj_stride & 15) &&
+        atlas_estimate(ctx->k, ctx->p, check) <= kAtlasHostFlagBytes) {
+        e = recon_dev_multi_atlas(ctx, d_base, present, shard_len, pitch, obj_stride, nobj,
+                                  check ? kAtlasDecode : data_only ? kAtlasData : kAtlasReconstruct, d_bad, stream);
+        if (e != RSGPU_ERR_NOT_IMPLEMENTED) return e;
+    }
     // pattern key: the present bitmask (n <= 64: one word, looked up in a
     // PatternTable — a Get batch of 4 KiB objects holds 10^5+ objects, and
     // this loop is host time in front of the launch; else a byte string)

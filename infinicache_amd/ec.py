@@ -226,6 +226,13 @@ class RSEncoder:
         self._L.rsgpu_devices(self._ctx, out, n)
         return list(out[:n])
 
+    def device_calls(self) -> List[int]:
+        """Compute calls each entry of devices() has run (how work spread)."""
+        n = self._L.rsgpu_device_calls(self._ctx, None, 0)
+        out = (ctypes.c_uint64 * max(n, 1))()
+        self._L.rsgpu_device_calls(self._ctx, out, n)
+        return list(out[:n])
+
     def matrix(self) -> np.ndarray:
         out = np.zeros((self.Shards, self.DataShards), dtype=np.uint8)
         _check(self._L.rsgpu_matrix(self._ctx, out.ctypes.data_as(_lib.u8p)))

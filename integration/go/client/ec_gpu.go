@@ -113,6 +113,21 @@ func newGPUEncoder(dataShards, parityShards int) (reedsolomon.Encoder, error) {
 	if rc != 0 {
 		return nil, rsErr(rc)
 	}
+	// No usable gfx950 device behind the context (RSGPU_ALL_DEVICES falls back
+	// to a device-0 context whose compute calls all fail): report an error so
+	// the patched NewEncoder keeps upstream's CPU coder (ADVICE r02).
+	{
+		var devs [256]C.int
+		nd := int(C.rsgpu_devices(ctx, &devs[0], 256))
+		usable := nd > 0
+		for i := 0; i < nd && i < 256 && usable; i++ {
+			usable = C.rsgpu_device_ok(devs[i]) == 1
+		}
+		if !usable {
+			C.rsgpu_destroy(ctx)
+			return nil, errors.New(C.GoString(C.rsgpu_strerror(C.RSGPU_ERR_NO_DEVICE)))
+		}
+	}
 	e := &gpuEncoder{ctx: ctx, DataShards: dataShards, ParityShards: parityShards,
 		Shards: dataShards + parityShards}
 	runtime.SetFinalizer(e, func(e *gpuEncoder) {

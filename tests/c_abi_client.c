@@ -65,7 +65,12 @@ static int host_checks(void) {
     CHECK(rsgpu_encode_image(ctx, a, 0, 12) == RSGPU_ERR_SHARD_NO_DATA);
     rsgpu_destroy(ctx);
     int devs[2] = {0, 0};
-    CHECK(rsgpu_create_multi(10, 2, devs, 2, 0, &ctx) == RSGPU_ERR_INVALID_ARG && ctx == NULL);
+    uint64_t calls[2] = {7, 7};
+    /* a device listed twice: two independent entries, no calls yet */
+    CHECK(rsgpu_create_multi(10, 2, devs, 2, 0, &ctx) == RSGPU_OK && rsgpu_devices(ctx, devs, 2) == 2);
+    CHECK(rsgpu_device_calls(ctx, calls, 2) == 2 && calls[0] == 0 && calls[1] == 0);
+    rsgpu_destroy(ctx);
+    CHECK(rsgpu_create_multi(10, 2, NULL, 2, 0, &ctx) == RSGPU_ERR_INVALID_ARG && ctx == NULL);
     CHECK(rsgpu_create(10, 2, RSGPU_ALL_DEVICES, 0, &ctx) == RSGPU_OK && rsgpu_devices(ctx, devs, 2) >= 1);
     rsgpu_destroy(ctx);
     printf("host checks ok (devices: %d)\n", rsgpu_device_count());

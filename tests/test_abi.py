@@ -174,14 +174,18 @@ def test_mixed_pattern_planning_without_device(k, p):
 
 def test_multi_device_context_host_side():
     """rsgpu_create_multi / RSGPU_ALL_DEVICES need no device to be created
-    (the matrix is host work); duplicates are rejected; compute calls without
-    a device fail loudly with ErrNoDevice, never on a CPU fallback."""
+    (the matrix is host work); a device listed twice gives two independent
+    entries; compute calls without a device fail loudly with ErrNoDevice,
+    never on a CPU fallback."""
     L = _lib.load()
     ctx = ctypes.c_void_p()
     devs = (ctypes.c_int * 2)(0, 0)
-    assert L.rsgpu_create_multi(10, 2, devs, 2, 0, ctypes.byref(ctx)) == -20  # duplicate device
+    assert L.rsgpu_create_multi(10, 2, devs, 0, 0, ctypes.byref(ctx)) == -20  # no devices
     assert not ctx.value
     assert L.rsgpu_create_multi(0, 2, devs, 1, 0, ctypes.byref(ctx)) == oracle.ERR_INV_SHARD_NUM
+    dup = ia.New(10, 2, devices=[0, 0, 0])
+    assert dup.devices() == [0, 0, 0]
+    assert dup.device_calls() == [0, 0, 0]
     enc = ia.New(10, 2, devices=[0])
     assert enc.devices() == [0]
     assert np.array_equal(enc.matrix(), ia.New(10, 2).matrix())

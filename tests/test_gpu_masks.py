@@ -271,6 +271,39 @@ def test_host_flags_route_through_masks(gpu):
         enc.decode_dev_multi(b, present, S, pitch, n * pitch, nobj, bad, s)
 
 
+@pytest.mark.parametrize("k,p", [(2, 14), (4, 12), (8, 8)])
+def test_host_flags_large_atlas_codes(gpu, k, p):
+    """n = 16 codes whose pattern atlas would be large (RS(2+14), RS(4+12):
+    ~65k patterns; RS(8+8): ~40k) keep the host-planned path for the host-flag
+    calls (they used to return ErrNotImplemented or build the
+    whole atlas on the first call).  Every object its own pattern, against
+    the encode's golden rows, plus ReconstructData."""
+    n = k + p
+    S, nobj = 1000, 60
+    pitch = _pitch(S)
+    rng = np.random.default_rng(k * 31 + p)
+    b = _batch(nobj, n, S, pitch, seed=k + 100 * p)
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.encode_dev(b, S, pitch, n * pitch, nobj, s)
+    golden = b.clone()
+    present = np.ones((nobj, n), dtype=np.uint8)
+    for o in range(nobj):
+        present[o, rng.choice(n, int(rng.integers(1, p + 1)), replace=False)] = 0
+        b[o, torch.as_tensor(np.flatnonzero(present[o] == 0), dtype=torch.long)] = 0x3C
+    bad = torch.full((nobj,), 4, dtype=torch.int32, device="cuda")
+    enc.decode_dev_multi(b, present, S, pitch, n * pitch, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert not bad.any()
+    assert torch.equal(b[:, :, :S], golden[:, :, :S])
+    for o in range(nobj):
+        b[o, torch.as_tensor(np.flatnonzero(present[o] == 0), dtype=torch.long)] = 0x3C
+    enc.reconstruct_dev_multi(b, present, S, pitch, n * pitch, nobj, data_only=True, stream=s)
+    torch.cuda.synchronize()
+    for o in range(nobj):
+        assert torch.equal(b[o, :k, :S], golden[o, :k, :S]), o
+
+
 def test_masks_wide_code_not_implemented(gpu):
     enc = ia.New(20, 4)
     b = torch.zeros((2, 24, 256), dtype=torch.uint8, device="cuda")

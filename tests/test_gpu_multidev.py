@@ -97,6 +97,141 @@ def test_multi_device_dev_calls_follow_the_memory(gpu):
         enc.encode_dev(hostbuf.ctypes.data, S, pitch, (k + p) * pitch, 1)
 
 
+@pytest.mark.parametrize("entries", [2, 3])
+def test_repeated_device_entries_every_forwarding_path(gpu, entries):
+    """N > 1 on the one-GPU test box: a context over device 0 listed N times
+    has N independent entries, so every multi-device forwarding path runs
+    with N > 1 (client/client.go:47-59, ecRedis.go:102-109 fan-out):
+    per-object round robin, the batch split o -> entry o mod N on N - 1 extra
+    host threads with the merged ok[], and device-resident calls routed by
+    the memory's owner (entries of one device in turn).  Every result
+    against the oracle; device_calls() shows each path reached each entry."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p, devices=[0] * entries)
+    assert enc.devices() == [0] * entries
+    m = enc.matrix()
+
+    def spread(before):
+        now = enc.device_calls()
+        return [a - b for a, b in zip(now, before)]
+
+    # per-object host calls: round robin over the entries
+    c0 = enc.device_calls()
+    for i, size in enumerate([1, 103, 4096, 104858, 77777, 5000]):
+        full = _full(k, p, size, 1200 + i)
+        sh = [full[j].copy() if j < k else np.zeros(size, np.uint8) for j in range(n)]
+        assert enc.EncodeVerify(sh)
+        for j in range(n):
+            assert np.array_equal(sh[j], full[j]), (size, j)
+        got = [None if j in (i % n, (i + 7) % n) else sh[j] for j in range(n)]
+        assert enc.DecodeVerify(got)
+        for j in range(n):
+            assert np.array_equal(got[j], full[j]), (size, j)
+    d = spread(c0)
+    assert all(x >= 12 // entries for x in d), d
+
+    # host batches: object o -> entry o mod N, one host thread per extra
+    # entry; object 4's parity is corrupted before decode, so its ok[] entry
+    # must come back False at index 4 whatever entry coded it
+    c0 = enc.device_calls()
+    sizes = [5, 4096, 1 << 20, 333, 70001, 17, 9999]
+    objs, fulls = [], []
+    for i, nb in enumerate(sizes):
+        data = rn.splitmix64_bytes(SEED, 1300 + i, nb)
+        sh = enc.Split(data)
+        S = len(sh[0])
+        buf = ia.host_alloc(n * S) if i % 2 else np.zeros(n * S, np.uint8)
+        buf[:] = np.concatenate(sh)
+        objs.append([buf[j * S:(j + 1) * S] for j in range(n)])
+        e, want = oracle.encode(k, p, [s.copy() for s in sh[:k]] + [bytes(S)] * p)
+        fulls.append(want)
+    enc.encode_batch(objs)
+    for sh, want in zip(objs, fulls):
+        for j in range(n):
+            assert np.array_equal(sh[j], want[j])
+    assert all(x >= 1 for x in spread(c0))
+    lost = [(0, 5), (1,), (2, 3), (), (4,), (10, 11), (6,)]
+    for o in range(len(sizes)):
+        for j in lost[o]:
+            objs[o][j][:] = 0xEE
+    objs[4][11][0] ^= 1  # extra present parity shard of object 4 disagrees
+    present = [[j not in lost[o] for j in range(n)] for o in range(len(sizes))]
+    ok = enc.decode_batch(objs, present=present)
+    assert ok == [o != 4 for o in range(len(sizes))], ok
+    for o, (sh, want) in enumerate(zip(objs, fulls)):
+        for j in range(n):
+            if not (o == 4 and j == 11):
+                assert np.array_equal(sh[j], want[j]), (o, j)
+
+    # device-resident calls: each on its own buffer, routed to the entries
+    # of device 0 in turn (sub_for), through the plain, host-flag and
+    # device-mask forms
+    c0 = enc.device_calls()
+    S, pitch, nobj = 3000, 3072, 5
+    s = torch.cuda.current_stream()
+    for t in range(2 * entries):
+        g = torch.Generator(device="cuda:0").manual_seed(40 + t)
+        b = torch.randint(0, 256, (nobj, n, pitch), dtype=torch.uint8, device="cuda:0", generator=g)
+        b[:, :, S:] = 0
+        enc.encode_dev(b, S, pitch, n * pitch, nobj, s)
+        torch.cuda.synchronize()
+        golden = b.clone()
+        h = golden.cpu().numpy()
+        for o in range(nobj):
+            want = oracle.apply(m[k:], [h[o, c, :S] for c in range(k)])
+            for r in range(p):
+                assert np.array_equal(h[o, k + r, :S], want[r])
+        pres = np.ones((nobj, n), np.uint8)
+        for o in range(nobj):
+            pres[o, [(o + t) % n, (o + t + 3) % n]] = 0
+        for o in range(nobj):
+            b[o, np.flatnonzero(pres[o] == 0)] = 0x5A
+        st = torch.full((nobj,), 9, dtype=torch.int32, device="cuda:0")
+        if t % 2:
+            masks = torch.from_numpy((pres.astype(np.int64) << np.arange(n)).sum(1).astype(np.int32)).cuda()
+            enc.decode_dev_masks(b, masks, S, pitch, n * pitch, nobj, st, s)
+        else:
+            enc.decode_dev_multi(b, pres, S, pitch, n * pitch, nobj, st, s)
+        torch.cuda.synchronize()
+        assert not st.any()
+        assert torch.equal(b[:, :, :S], golden[:, :, :S]), t
+    d = spread(c0)
+    assert all(x >= 2 for x in d), d
+
+
+def test_repeated_entries_concurrent_callers(gpu):
+    """Several host threads on one 3-entry context: per-object calls spread
+    over the entries' own slot pools and streams concurrently."""
+    import threading
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p, devices=[0, 0, 0])
+    errors = []
+
+    def caller(tid):
+        try:
+            for i in range(6):
+                size = 1000 + 97 * tid + i
+                full = _full(k, p, size, 1400 + tid * 10 + i)
+                sh = [full[j].copy() if j < k else np.zeros(size, np.uint8) for j in range(n)]
+                assert enc.EncodeVerify(sh)
+                got = [None if j in (tid % n, (i + 4) % n) else sh[j] for j in range(n)]
+                assert enc.DecodeVerify(got)
+                for j in range(n):
+                    assert np.array_equal(got[j], full[j])
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=caller, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors
+    assert all(x > 0 for x in enc.device_calls())
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_trace_pipeline_config5_sizes(gpu, pinned):
     """encode_batch + decode_batch over a small log-uniform trace: 4 KiB

@@ -1,0 +1,229 @@
+// mailbox_probe.hip — host <-> GPU round-trip latency of the transports a
+// resident per-object worker could use (DESIGN.md §6 "Per-object latency").
+//
+//   ./mailbox_probe [iters]
+//
+// launch   : empty kernel launch + hipStreamSynchronize (the per-call floor of
+//            the stream path)
+// hostpoll : a resident kernel (one workgroup) polls a word in coherent
+//            pinned host memory; per request it reads 10 rows of a 1 KiB
+//            RS(10+2) object (S = 103) from pinned host memory over PCIe,
+//            XORs them into 2 rows, stores those into host memory and
+//            publishes the request's sequence number.  Variants: the flag
+//            published by a system-scope release store, or by write-through
+//            (sc0 sc1) row stores + vmcnt(0) + a plain system-scope store.
+// devpoll  : the same with the doorbell in fine-grained device memory written
+//            by the host through the BAR (only if the runtime reports a host
+//            mapping for it).
+// Every kernel has an exit every wave reaches: a stop word, and an idle
+// limit on the device's real-time clock.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(1);                                                                      \
+        }                                                                                      \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct Mailbox {           // one cache line per direction
+    uint32_t seq;          // host -> GPU doorbell (request number)
+    uint32_t stop;
+    uint32_t S, pad;
+    uint64_t in, out;      // device addresses of the host rows
+    uint32_t pad2[8];
+    uint32_t resp;         // GPU -> host: last request done
+    uint32_t pad3[15];
+};
+
+constexpr int kSys = 1 | 16;  // buffer-op cache policy: sc0 | sc1 (system coherent)
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// VARIANT 0: release store of the flag; 1: write-through rows + vmcnt(0) + relaxed flag
+template <int VARIANT, int SLEEP>
+__global__ __launch_bounds__(256) void worker(Mailbox *mb, uint32_t *bell, uint64_t idle_ticks) {
+    __shared__ uint32_t s_seq;
+    const uint32_t t = threadIdx.x;
+    uint32_t last = 0;
+    for (;;) {
+        if (t == 0) {
+            uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t s;
+            for (;;) {
+                s = ld_sys(bell);
+                if (s != last) break;
+                if (ld_sys(&mb->stop)) { s = 0xffffffffu; break; }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) { s = 0xffffffffu; break; }
+                if (SLEEP) __builtin_amdgcn_s_sleep(SLEEP);
+            }
+            s_seq = s;
+        }
+        __syncthreads();
+        const uint32_t s = s_seq;
+        __syncthreads();
+        if (s == 0xffffffffu) return;
+        last = s;
+        const uint32_t S = ld_sys(&mb->S);
+        const uint8_t *in = (const uint8_t *)ld_sys64(&mb->in);
+        uint8_t *out = (uint8_t *)ld_sys64(&mb->out);
+        const uint32_t nvec = (S + 15) / 16;
+        const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)(12 * S + 64), 0x00020000);
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)(2 * nvec * 16), 0x00020000);
+        if (t < nvec) {
+            u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+            u32x4 x[10];
+#pragma unroll
+            for (int c = 0; c < 10; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(ri, t * 16, c * S, kSys);
+#pragma unroll
+            for (int c = 0; c < 10; ++c) {
+                a ^= x[c];
+                if (c & 1) b ^= x[c];
+            }
+            // output rows at a 16-B padded pitch (whole-vector stores)
+            __builtin_amdgcn_raw_buffer_store_b128(a, ro, t * 16, 0, VARIANT ? kSys : 0);
+            __builtin_amdgcn_raw_buffer_store_b128(b, ro, t * 16, nvec * 16, VARIANT ? kSys : 0);
+        }
+        if (VARIANT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            if (VARIANT)
+                __hip_atomic_store(&mb->resp, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            else
+                __hip_atomic_store(&mb->resp, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+__global__ void empty_kernel(int *p) {
+    if (p && threadIdx.x == 1000) *p = 1;
+}
+
+static double pct(std::vector<double> v, double p) {
+    std::sort(v.begin(), v.end());
+    return v[(size_t)(p * (v.size() - 1) + 0.5)];
+}
+
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <int VARIANT, int SLEEP>
+static void run_poll(const char *name, bool devbell, int iters) {
+    Mailbox *mb = nullptr, *dmb = nullptr;
+    CK(hipHostMalloc((void **)&mb, sizeof(Mailbox), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(mb, 0, sizeof(Mailbox));
+    CK(hipHostGetDevicePointer((void **)&dmb, mb, 0));
+    uint32_t *bell_host = &mb->seq, *bell_dev = &dmb->seq;
+    uint32_t *fg = nullptr;
+    if (devbell) {
+        hipError_t e = hipExtMallocWithFlags((void **)&fg, 4096, hipDeviceMallocFinegrained);
+        if (e != hipSuccess) {
+            std::printf("%s: hipExtMallocWithFlags(finegrained) failed: %s\n", name, hipGetErrorString(e));
+            return;
+        }
+        hipPointerAttribute_t at;
+        CK(hipPointerGetAttributes(&at, fg));
+        std::printf("%s: finegrained device memory: type %d device %d hostPointer %p devicePointer %p\n", name,
+                    (int)at.type, at.device, at.hostPointer, at.devicePointer);
+        if (!at.hostPointer) {
+            std::printf("%s: no host mapping reported: skipped\n", name);
+            (void)hipFree(fg);
+            return;
+        }
+        bell_host = (uint32_t *)at.hostPointer;
+        bell_dev = fg;
+        *(volatile uint32_t *)bell_host = 0;
+    }
+    const uint32_t S = 103;
+    uint8_t *in = nullptr, *out = nullptr, *din = nullptr, *dout = nullptr;
+    CK(hipHostMalloc((void **)&in, 12 * S + 64, hipHostMallocDefault));
+    CK(hipHostMalloc((void **)&out, 2 * 112 + 64, hipHostMallocDefault));
+    CK(hipHostGetDevicePointer((void **)&din, in, 0));
+    CK(hipHostGetDevicePointer((void **)&dout, out, 0));
+    mb->S = S;
+    mb->in = (uint64_t)din;
+    mb->out = (uint64_t)dout;
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipLaunchKernelGGL((worker<VARIANT, SLEEP>), dim3(1), dim3(256), 0, st, dmb, bell_dev, (uint64_t)200000000);  // 2 s idle
+    CK(hipGetLastError());
+    std::vector<double> lat;
+    int bad = 0;
+    uint8_t want[2][112];
+    for (int it = 1; it <= iters; ++it) {
+        for (uint32_t i = 0; i < 12 * S; ++i) in[i] = (uint8_t)(i * 7 + it * 13);
+        for (uint32_t j = 0; j < S; ++j) {
+            uint8_t a = 0, b = 0;
+            for (int c = 0; c < 10; ++c) {
+                a ^= in[c * S + j];
+                if (c & 1) b ^= in[c * S + j];
+            }
+            want[0][j] = a;
+            want[1][j] = b;
+        }
+        const double t0 = now_us();
+        __atomic_store_n(bell_host, (uint32_t)it, __ATOMIC_RELEASE);
+        while (__atomic_load_n(&mb->resp, __ATOMIC_ACQUIRE) != (uint32_t)it) {
+            if (now_us() - t0 > 1e6) {
+                std::printf("%s: no response after 1 s at request %d\n", name, it);
+                mb->stop = 1;
+                CK(hipStreamSynchronize(st));
+                return;
+            }
+        }
+        const double t1 = now_us();
+        if (std::memcmp(out, want[0], S) || std::memcmp(out + 112, want[1], S)) ++bad;
+        lat.push_back(t1 - t0);
+    }
+    mb->stop = 1;
+    CK(hipStreamSynchronize(st));
+    std::printf("%-34s p50 %6.2f us  p90 %6.2f  p99 %6.2f  min %6.2f  (%d iters, %d wrong)\n", name, pct(lat, 0.5),
+                pct(lat, 0.9), pct(lat, 0.99), pct(lat, 0.0), iters, bad);
+    CK(hipStreamDestroy(st));
+    (void)hipHostFree(in);
+    (void)hipHostFree(out);
+    (void)hipHostFree(mb);
+    if (fg) (void)hipFree(fg);
+}
+
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+    CK(hipSetDevice(0));
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    {
+        std::vector<double> lat;
+        for (int i = 0; i < iters + 50; ++i) {
+            const double t0 = now_us();
+            hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, st, nullptr);
+            CK(hipStreamSynchronize(st));
+            if (i >= 50) lat.push_back(now_us() - t0);
+        }
+        std::printf("%-34s p50 %6.2f us  p90 %6.2f  p99 %6.2f  min %6.2f\n", "launch+sync (empty kernel)",
+                    pct(lat, 0.5), pct(lat, 0.9), pct(lat, 0.99), pct(lat, 0.0));
+    }
+    run_poll<0, 1>("hostpoll release-flag sleep1", false, iters);
+    run_poll<1, 1>("hostpoll wt-rows+flag sleep1", false, iters);
+    run_poll<1, 0>("hostpoll wt-rows+flag nosleep", false, iters);
+    run_poll<1, 4>("hostpoll wt-rows+flag sleep4", false, iters);
+    run_poll<1, 1>("devpoll wt-rows+flag sleep1", true, iters);
+    return 0;
+}
