@@ -388,20 +388,50 @@ def run_trace(args):
     pres = [i not in lost for i in range(n)]
     bad = torch.zeros(1, dtype=torch.int32, device="cuda")
 
-    def dstep():
+    def dstep_per_object():  # round 2's form: one launch per object and op
         for o in range(nobj):
             b = dev.data_ptr() + int(doffs[o])
             enc.encode_dev(b, int(S[o]), pitches[o], n * pitches[o], 1, stream)
             enc.decode_dev(b, pres, int(S[o]), pitches[o], n * pitches[o], 1, bad, stream)
 
-    dstep()
+    # one launch per op over the whole trace (variable-size table)
+    dobjs = [(dev.data_ptr() + int(doffs[o]), int(S[o]), pitches[o]) for o in range(nobj)]
+    badv = torch.zeros(nobj, dtype=torch.int32, device="cuda")
+
+    def dstep():
+        enc.encode_dev_objs(dobjs, stream)
+        enc.decode_dev_objs(dobjs, pres, badv, stream)
+
+    def time_dev(fn):
+        fn()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t1
+
+    # device-resident work check: garbage into the lost rows of every object,
+    # one decode, compare with the rows before
+    dgen = torch.Generator(device="cuda").manual_seed(3)
+    dev.copy_(torch.randint(0, 256, dev.shape, dtype=torch.uint8, device="cuda", generator=dgen))
+    enc.encode_dev_objs(dobjs, stream)
+    ref = dev.clone()
+    for o in range(nobj):
+        for i in lost:
+            a = int(doffs[o]) + i * pitches[o]
+            dev[a:a + int(S[o])] = 0xA5
+    badv.fill_(7)
+    enc.decode_dev_objs(dobjs, pres, badv, stream)
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        dstep()
-    torch.cuda.synchronize()
-    dev_el = time.perf_counter() - t1
+    dev_check = "bit-exact" if (not bool(badv.any()) and torch.equal(dev, ref)) else "MISMATCH"
+    del ref
+    if dev_check != "bit-exact":
+        raise SystemExit("trace device-resident decode check failed")
+    dev_el = time_dev(dstep)
     dev_rate = 2 * total_obj * args.steps / dev_el / GiB
+    per_obj_el = time_dev(dstep_per_object)
+    per_obj_rate = 2 * total_obj * args.steps / per_obj_el / GiB
 
     cpu = None
     if not args.no_cpu:
@@ -443,6 +473,10 @@ def run_trace(args):
                    "size_min": int(sizes.min()), "size_max": int(sizes.max()),
                    "size_median": int(np.median(sizes))},
         "device_resident_same_trace_GiBps": round(dev_rate, 2),
+        "device_resident_form": "rsgpu_encode_dev_objs + rsgpu_decode_dev_objs: one launch per op "
+                                "over the whole trace (variable-size object table)",
+        "device_resident_check": dev_check,
+        "device_resident_per_object_launches_GiBps": round(per_obj_rate, 2),
         "kernel_fraction_of_e2e_time": round(dev_el / el, 4),
         "cpu_baseline": cpu,
     }

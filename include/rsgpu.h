@@ -148,6 +148,38 @@ int rsgpu_decode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
 int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int nshards,
                  const uint8_t *const *newdata, const size_t *new_lens, int nnew);
 
+/* ---- resident worker: low-latency per-object calls -----------------------
+ * One EcSet / EcGet codes ONE object (ecRedis.go:96, :173; the example object
+ * is 1 KiB, client/example/main.go:15,26).  On the stream path each such call
+ * costs a kernel launch plus a stream synchronisation (>= 10.8 us on MI355X
+ * for an empty kernel).  rsgpu_worker_start makes the per-object calls above
+ * (rsgpu_encode, rsgpu_encode_verify, rsgpu_verify, rsgpu_reconstruct,
+ * rsgpu_decode and their *_image forms) go to a resident kernel instead:
+ * nslots workgroups, each polling its own request mailbox in pinned host
+ * memory; a call posts one 64-B request line and spins on the response word.
+ * The object's rows are read and written over PCIe in place when they form
+ * one Split image in memory from rsgpu_host_alloc, else through the mailbox's
+ * pinned image (memcpy).  Objects with shard_len > max_shard, codes of more
+ * than 16 shards, and calls that find every mailbox busy take the stream path.
+ * Results, checks and errors are exactly those of the stream path.
+ *   nslots     mailboxes = resident workgroups (1..64; 0: 8)
+ *   idle_us    the kernel leaves after this long without any request (0: 50 ms)
+ *              and the next call relaunches it; while it runs, a
+ *              hipDeviceSynchronize in the process waits for it to leave
+ *   max_shard  the largest shard_len served (0: 16 KiB)
+ * Calling it again restarts the worker with the new settings.  Multi-device
+ * contexts: one worker per entry.  Requires data+parity <= 16
+ * (RSGPU_ERR_NOT_IMPLEMENTED otherwise). */
+int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard);
+/* Stops the worker (waits for calls in flight); the per-object calls go back
+ * to the stream path.  rsgpu_destroy stops it too. */
+int rsgpu_worker_stop(rsgpu_ctx *ctx);
+/* Calls the worker served, calls it declined because every mailbox was busy
+ * (they took the stream path), and kernel launches so far (the first call
+ * after an idle exit relaunches it); summed over a multi-device context's
+ * entries.  Any pointer may be NULL. */
+int rsgpu_worker_stats(const rsgpu_ctx *ctx, uint64_t *served, uint64_t *declined, uint64_t *launches);
+
 /* ---- per-object calls on one contiguous image ----------------------------
  * Shard i of the object is base[i*shard_len, (i+1)*shard_len): Split's layout
  * (ecRedis.go:384 — Split returns consecutive slices of one backing array).
@@ -237,6 +269,29 @@ int rsgpu_decode_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks
 int rsgpu_reconstruct_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len,
                                 size_t pitch, size_t obj_stride, int nobj, int data_only,
                                 uint32_t *d_status, void *stream);
+
+/* ---- variable-size device-resident batches ------------------------------
+ * Objects of ANY sizes in one launch per pass (config 5's objects range from
+ * 4 KiB to 100 MiB, client/ecRedis.go:96): objs[o] (a host array) describes
+ * object o, shard i at base + i*pitch with pitch >= shard_len rounded up to
+ * 16 (so no row's last 16-B vector reaches past the object's data+parity
+ * rows); (data+parity)*pitch < 4 GiB.  Every object in device memory of one
+ * device.  The table is uploaded by the library (a pinned ring, no per-call
+ * allocation); the calls are asynchronous on `stream` like the *_dev calls,
+ * with the same per-object semantics; d_bad[o] refers to objs[o]. */
+typedef struct rsgpu_dev_obj {
+    void *base;       /* device address of shard 0 of the object */
+    size_t shard_len; /* bytes per shard of this object */
+    size_t pitch;     /* bytes between its shard rows */
+} rsgpu_dev_obj;
+
+int rsgpu_encode_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, void *stream);
+int rsgpu_verify_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, uint32_t *d_bad, void *stream);
+/* one erasure pattern for every object: present[i] != 0 marks row i present */
+int rsgpu_reconstruct_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, const uint8_t *present,
+                               int data_only, void *stream);
+int rsgpu_decode_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, const uint8_t *present,
+                          uint32_t *d_bad, void *stream);
 
 /* ---- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
  * The path starts and ends in host memory (ecRedis.go:96 Set buffer,

@@ -25,6 +25,8 @@ EXPORTS = (
     "rsgpu_encode_verify", "rsgpu_decode_dev_masks", "rsgpu_reconstruct_dev_masks",
     "rsgpu_create_multi", "rsgpu_devices", "rsgpu_encode_image", "rsgpu_encode_verify_image",
     "rsgpu_verify_image", "rsgpu_reconstruct_image", "rsgpu_decode_image", "rsgpu_device_calls",
+    "rsgpu_encode_dev_objs", "rsgpu_verify_dev_objs", "rsgpu_reconstruct_dev_objs", "rsgpu_decode_dev_objs",
+    "rsgpu_worker_start", "rsgpu_worker_stop", "rsgpu_worker_stats",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -36,6 +38,11 @@ sz = ctypes.c_size_t
 ci = ctypes.c_int
 
 _lib = None
+
+
+class DevObj(ctypes.Structure):
+    """rsgpu_dev_obj: one object of a variable-size device batch."""
+    _fields_ = [("base", ctypes.c_void_p), ("shard_len", ctypes.c_size_t), ("pitch", ctypes.c_size_t)]
 
 
 class LibraryMissing(RuntimeError):
@@ -94,6 +101,14 @@ def load():
     L.rsgpu_verify_image.argtypes = [vp, vp, sz, ci, intp]
     L.rsgpu_reconstruct_image.argtypes = [vp, vp, sz, ci, ctypes.c_uint64, ci]
     L.rsgpu_decode_image.argtypes = [vp, vp, sz, ci, ctypes.c_uint64, intp]
+    L.rsgpu_encode_dev_objs.argtypes = [vp, vp, ci, vp]
+    L.rsgpu_verify_dev_objs.argtypes = [vp, vp, ci, vp, vp]
+    L.rsgpu_reconstruct_dev_objs.argtypes = [vp, vp, ci, u8p, ci, vp]
+    L.rsgpu_decode_dev_objs.argtypes = [vp, vp, ci, u8p, vp, vp]
+    L.rsgpu_worker_start.argtypes = [vp, ci, ctypes.c_uint, sz]
+    L.rsgpu_worker_stop.argtypes = [vp]
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    L.rsgpu_worker_stats.argtypes = [vp, u64p, u64p, u64p]
     L.rsgpu_encode_batch.argtypes = [vp, u8pp, szp, ci]
     L.rsgpu_decode_batch.argtypes = [vp, u8pp, u8p, szp, ci, intp]
     L.rsgpu_host_register.argtypes = [vp, sz]

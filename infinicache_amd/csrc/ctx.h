@@ -127,6 +127,13 @@ struct Atlas {
 size_t atlas_estimate(int k, int p, bool check);
 enum AtlasMode { kAtlasReconstruct = 0, kAtlasData = 1, kAtlasDecode = 2 };
 
+// The resident per-object coder (gf_worker.hip, rsgpu_worker_start).
+struct Worker;
+struct WorkerDeleter {
+    void operator()(Worker *w) const;
+};
+constexpr int kWorkerDeclined = 1;  // worker_run: not served here, take the stream path
+
 }  // namespace rsgpu
 
 using namespace rsgpu;
@@ -138,6 +145,8 @@ struct rsgpu_ctx {
     uint32_t *d_ctab = nullptr;      // [256][8] coefficient tables (gf_apply_lanes)
     std::mutex ctab_mu;              // guards the d_ctab upload (retried after a failure)
     rsgpu::StatusScratch scratch;    // multi-reporter status of the masked decode
+    std::unique_ptr<rsgpu::Worker, rsgpu::WorkerDeleter> worker;  // rsgpu_worker_start (nullptr: off)
+    std::mutex worker_mu;            // starts and stops
     // Multi-device context (rsgpu_create_multi / RSGPU_ALL_DEVICES): one
     // single-device context per entry of the device list.  Per-object calls
     // go round-robin, batch calls split objects o -> entry o mod N and run the
@@ -399,4 +408,11 @@ bool host_pinned(const void *p, size_t len);
 // the device address of such a range (kernels read/write it over PCIe), or
 // nullptr when [p, p+len) is not inside one pinned range
 void *host_device_ptr(const void *p, size_t len);
+// One object through the resident worker (gf_worker.hip): rows[0..n) the
+// object's shards (every one a buffer of S bytes; missing ones receive their
+// reconstruction), mask the present rows (reconstruct / decode).  RSGPU_OK
+// with *bad = 0 / 1 (a check failed), kWorkerDeclined (no worker, too large,
+// every mailbox busy: the caller takes the stream path) or an error.
+int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *const *rows, uint32_t *bad);
+int worker_stop(rsgpu_ctx *ctx);
 }  // namespace rsgpu

@@ -125,6 +125,19 @@ hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vecto
                               const Layout &L, uint32_t *d_bad, hipStream_t stream,
                               MultiWorkspace &ws);
 
+// One object of a variable-size device batch (rsgpu_*_dev_objs): shard i at
+// base + i * pitch, pitch >= roundup16(shard_len) (no row's last vector
+// reaches past the object's rows).
+struct DevObj {
+    uint8_t *base;
+    size_t shard_len, pitch;
+};
+// Codes every object of the table with the plan, one launch per sub-pass of
+// <= 4 rows whatever the objects' sizes (the table goes up through ws's
+// ring).  d_bad[o] follows launch_plan's contract per object.
+hipError_t launch_plan_objs(Plan &p, const DevObj *objs, int nobj, uint32_t *d_bad, hipStream_t stream,
+                            MultiWorkspace &ws);
+
 // Launches the plan over all objects on `stream`.  d_bad (nobj u32) must be
 // zeroed by the caller when the plan has check rows.  Returns hipSuccess or
 // the first HIP error.

@@ -187,11 +187,15 @@ struct Redirect {
 // objects, lane -> (object, vector); `ob` is then the first object's base
 // (uniform), `lane_off` the lane's object offset from it and `span` the bytes
 // the group's objects cover.
-template <int K, int R, int U, int BS, int LAUX, int SAUX, typename P>
+// Variable-size batches (VAR = true, gf_apply_var): the pass's in_off /
+// out_off hold row INDICES, scaled by the object's own pitch `vp`; `span` is
+// the object's own span and `vpacked` its store_row part.
+template <int K, int R, int U, int BS, int LAUX, int SAUX, typename P, bool VAR = false>
 __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P &a,
                                               uint32_t nvec, uint32_t tail, uint32_t *bad,
                                               uint32_t v0, const Redirect &rd = Redirect(),
-                                              uint32_t lane_off = 0, uint32_t span = 0) {
+                                              uint32_t lane_off = 0, uint32_t span = 0,
+                                              uint32_t vp = 0, uint32_t vpacked = 0) {
     if (v0 >= nvec) return;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)ob, (short)0, (int)(span ? span : a.span), 0x00020000);
@@ -200,6 +204,9 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
     const __amdgpu_buffer_rsrc_t rso =
         rd.out ? __builtin_amdgcn_make_buffer_rsrc((void *)rd.out, (short)0, (int)a.span, 0x00020000) : rs;
 
+    auto in_off = [&](int c) -> uint32_t { return VAR ? a.in_off[c] * vp : a.in_off[c]; };
+    auto out_off = [&](int r) -> uint32_t { return VAR ? a.out_off[r] * vp : a.out_off[r]; };
+    const uint32_t packed = VAR ? vpacked : a.packed;
     u32x4 x[U][K];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -207,11 +214,11 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         if (U == 1 || v < nvec) {
 #pragma unroll
             for (int c = 0; c < K; ++c)
-                x[u][c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, lane_off + v * 16u, a.in_off[c], LAUX);
+                x[u][c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, lane_off + v * 16u, in_off(c), LAUX);
             if (rd.copy_in) {
 #pragma unroll
                 for (int c = 0; c < K; ++c)
-                    store_row<SAUX>(x[u][c], rs, lane_off + v * 16u, a.in_off[c], v == nvec - 1 ? a.packed : 0u);
+                    store_row<SAUX>(x[u][c], rs, lane_off + v * 16u, in_off(c), v == nvec - 1 ? packed : 0u);
             }
         }
     }
@@ -254,8 +261,8 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         for (int r = 0; r < R; ++r) {
             if ((uint32_t)r < a.nw) {
                 u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                store_row<SAUX>(o, rso, lane_off + v * 16u, a.out_off[r], v == nvec - 1 ? a.packed : 0u);
-                if (rd.dual) store_row<SAUX>(o, rs, lane_off + v * 16u, a.out_off[r], v == nvec - 1 ? a.packed : 0u);
+                store_row<SAUX>(o, rso, lane_off + v * 16u, out_off(r), v == nvec - 1 ? packed : 0u);
+                if (rd.dual) store_row<SAUX>(o, rs, lane_off + v * 16u, out_off(r), v == nvec - 1 ? packed : 0u);
             } else {
                 const uint32_t valid = (v == nvec - 1) ? tail : 16u;
 #pragma unroll
@@ -325,13 +332,56 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
                                            a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd);
 }
 
+// constant address space: uniform invariant data the compiler may (and does)
+// fetch with scalar loads
+template <typename T>
+using constant_ptr = const __attribute__((address_space(4))) T *;
+
+// One object of a variable-size batch (rsgpu_*_dev_objs): a device table
+// entry, read by scalar loads.  chunk0 = the object's first workgroup in the
+// launch's flattened (object, chunk) space; the entries are in chunk0 order.
+struct VarObj {
+    uint64_t base;
+    uint32_t nvec, tail, pitch, span, packed, chunk0;
+};
+static_assert(sizeof(VarObj) == 32, "VarObj: one 32-B table entry");
+
+template <int K, int R>
+struct VarArgs {  // one pass over objects of different sizes and pitches (kernarg)
+    const VarObj *objs;
+    uint32_t nobj;
+    uint32_t *bad;   // per object (index into objs), or nullptr
+    Order ord;       // item = flattened chunk (nchunk = 1)
+    Pass<K, R> p;    // in_off / out_off: row indices (scaled by each object's pitch)
+};
+
+// Workgroup w codes chunk w - chunk0 of the object whose chunk range holds w,
+// found by a binary search over the table's chunk0 (uniform scalar loads that
+// hit the scalar cache after the first workgroups of the launch).
+template <int K, int R, int BS, int LAUX, int SAUX>
+__global__ __launch_bounds__(BS) void gf_apply_var(const VarArgs<K, R> a) {
+    uint32_t w, unused;
+    if (!wg_item(a.ord, w, unused)) return;
+    const constant_ptr<VarObj> objs = (constant_ptr<VarObj>)a.objs;
+    uint32_t lo = 0, hi = a.nobj;  // objs[lo].chunk0 <= w < objs[hi].chunk0
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (objs[mid].chunk0 <= w) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t base = objs[lo].base;
+    const uint32_t nvec = objs[lo].nvec, tail = objs[lo].tail, pitch = objs[lo].pitch;
+    const uint32_t span = objs[lo].span, packed = objs[lo].packed, c0 = objs[lo].chunk0;
+    gf_apply_body<K, R, 1, BS, LAUX, SAUX, const Pass<K, R>, true>(
+        (const uint8_t *)base, lo, a.p, nvec, tail, a.bad, (w - c0) * BS + threadIdx.x, Redirect(), 0u, span,
+        pitch, packed);
+}
+
 // Mixed erasure patterns in one launch: each workgroup reads its object's
 // pass index (uniform) and then the pass itself through scalar loads.  CH > 1
 // walks several chunks of the object per workgroup with the pass kept in
 // SGPRs; the product uses CH = 1 (the lookups cost nothing measurable,
 // tools/kbench KB_SET=multi, and longer walks were slower).
-template <typename T>
-using constant_ptr = const __attribute__((address_space(4))) T *;
 
 template <int K, int R, int U, int BS, int LAUX, int SAUX, int CH>
 __global__ __launch_bounds__(BS) void gf_apply_multi(const MultiArgs<K, R> m) {

@@ -808,6 +808,7 @@ MultiWorkspace::~MultiWorkspace() {
 
 hipError_t launch_plans_multi_core(const std::vector<Plan *> &plans, const std::vector<int> &plan_of,
                                    const Layout &L, uint32_t *d_bad, hipStream_t st, MultiWorkspace &ws);
+hipError_t stage_image(MultiWorkspace &ws, const std::vector<uint8_t> &img, MultiWorkspace::Slot *&out);
 
 hipError_t launch_plans_multi(const std::vector<Plan *> &plans, const std::vector<int> &plan_of,
                               const Layout &L, uint32_t *d_bad, hipStream_t st, MultiWorkspace &ws) {
@@ -860,6 +861,22 @@ hipError_t launch_plans_multi_core(const std::vector<Plan *> &plans, const std::
     for (auto &kv : classes)
         launches.emplace_back(0, pick_stage(kv.first.first, kv.first.second)(kv.second, L, d_bad, img));
     std::lock_guard<std::mutex> g(ws.mu);
+    MultiWorkspace::Slot *w = nullptr;
+    hipError_t e = stage_image(ws, img, w);
+    for (auto &l : launches)
+        if (e == hipSuccess) e = l.second((const uint8_t *)w->d, st);
+    if (e == hipSuccess) e = hipEventRecord(w->done, st);
+    return e;
+}
+
+// The next ring slot of ws holding `img` in device memory (ws.mu held).
+// The upload runs on its own stream and the HOST waits for it: the host is
+// normally several calls ahead of the GPU (the slot ring throttles it), so
+// the wait costs the GPU nothing.  Measured against a GPU-side
+// hipStreamWaitEvent and against a copy in the caller's stream: 1 % and 3.5 %
+// slower on the mixed bench (rocprof gaps).  The caller records
+// w->done on its stream after the kernels that read the image.
+hipError_t stage_image(MultiWorkspace &ws, const std::vector<uint8_t> &img, MultiWorkspace::Slot *&out) {
     MultiWorkspace::Slot &w = ws.slot[ws.next++ % MultiWorkspace::kRing];
     hipError_t e = hipSuccess;
     if (!ws.upload) {
@@ -886,16 +903,92 @@ hipError_t launch_plans_multi_core(const std::vector<Plan *> &plans, const std::
         w.cap = cap;
     }
     std::memcpy(w.h, img.data(), img.size());
-    // upload on its own stream and wait for it on the HOST: the host is
-    // normally several calls ahead of the GPU (the slot ring throttles it),
-    // so the wait costs the GPU nothing.  Measured against a GPU-side
-    // hipStreamWaitEvent and against a copy in the caller's stream: 1 % and
-    // 3.5 % slower on the mixed bench (rocprof gaps).
     e = hipMemcpyAsync(w.d, w.h, img.size(), hipMemcpyHostToDevice, ws.upload);
     if (e == hipSuccess) e = hipStreamSynchronize(ws.upload);
-    for (auto &l : launches)
-        if (e == hipSuccess) e = l.second((const uint8_t *)w.d, st);
-    if (e == hipSuccess) e = hipEventRecord(w.done, st);
+    out = &w;
+    return e;
+}
+
+// ---- variable-size batches (rsgpu_*_dev_objs): one launch per sub-pass over
+// objects of any sizes and pitches, the object table uploaded once per call
+
+namespace {
+
+template <int K, int R>
+hipError_t launch_var_t(const Plan &p, const Sub &s, const VarObj *d_objs, uint32_t nobj, uint32_t total,
+                        uint32_t *d_bad, hipStream_t st) {
+    VarArgs<K, R> a;
+    a.objs = d_objs;
+    a.nobj = nobj;
+    a.bad = d_bad;
+    // row indices, not offsets: pitch 1 (each object's pitch scales them in the kernel)
+    fill_pass<K, R>(p, s, 1, 16, 1, d_bad != nullptr, a.p);
+    unsigned grid;
+    a.ord = make_order(1, total, (size_t)1 << 40, grid);
+    hipLaunchKernelGGL((gf_apply_var<K, R, kBlock, kLoadAux, kStoreAux>), dim3(grid), dim3(kBlock),
+                       a.p.nw ? store_lds(K) : 0u, st, a);
+    return hipGetLastError();
+}
+
+typedef hipError_t (*var_fn)(const Plan &, const Sub &, const VarObj *, uint32_t, uint32_t, uint32_t *,
+                             hipStream_t);
+template <int K>
+var_fn pick_var_r(int R) {
+    return R == 1 ? &launch_var_t<K, 1> : R == 2 ? &launch_var_t<K, 2> : R == 3 ? &launch_var_t<K, 3>
+                                                                            : &launch_var_t<K, 4>;
+}
+var_fn pick_var(int K, int R) {
+    switch (K) {
+#define RSGPU_K(k) case k: return pick_var_r<k>(R);
+        RSGPU_K(1) RSGPU_K(2) RSGPU_K(3) RSGPU_K(4) RSGPU_K(5) RSGPU_K(6) RSGPU_K(7) RSGPU_K(8)
+        RSGPU_K(9) RSGPU_K(10) RSGPU_K(11) RSGPU_K(12) RSGPU_K(13) RSGPU_K(14) RSGPU_K(15)
+        RSGPU_K(16)
+#undef RSGPU_K
+        default: return nullptr;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_plan_objs(Plan &p, const DevObj *objs, int nobj, uint32_t *d_bad, hipStream_t st,
+                            MultiWorkspace &ws) {
+    if (nobj <= 0 || p.R <= 0) return hipSuccess;
+    if (p.K > kMaxK) {  // the generic kernel has no table form: object by object
+        for (int o = 0; o < nobj; ++o) {
+            Layout one{objs[o].base, 0, objs[o].pitch, objs[o].shard_len, 1};
+            hipError_t e = launch_plan(p, one, d_bad ? d_bad + o : nullptr, st);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    int maxrow = 0;
+    for (int r : p.in_rows) maxrow = std::max(maxrow, r);
+    for (int r : p.out_rows) maxrow = std::max(maxrow, r);
+    std::vector<uint8_t> img((size_t)nobj * sizeof(VarObj));
+    VarObj *t = (VarObj *)img.data();
+    uint64_t total = 0;
+    for (int o = 0; o < nobj; ++o) {
+        const DevObj &d = objs[o];
+        VarObj &v = t[o];
+        v.base = (uint64_t)d.base;
+        v.nvec = (uint32_t)((d.shard_len + 15) / 16);
+        v.tail = (uint32_t)(d.shard_len - (size_t)(v.nvec - 1) * 16);
+        v.pitch = (uint32_t)d.pitch;
+        v.span = (uint32_t)((size_t)maxrow * d.pitch + (size_t)v.nvec * 16);
+        v.packed = tail_part(d.pitch, v.nvec);
+        v.chunk0 = (uint32_t)total;
+        total += (v.nvec + kBlock - 1) / kBlock;
+    }
+    if (total >= 0x7ff00000ull) return hipErrorInvalidValue;  // > 2^31 workgroups: split the table
+    std::lock_guard<std::mutex> g(ws.mu);
+    MultiWorkspace::Slot *w = nullptr;
+    hipError_t e = stage_image(ws, img, w);
+    for (int r0 = 0; r0 < p.R && e == hipSuccess; r0 += kMaxR) {
+        Sub s{r0, std::min(kMaxR, p.R - r0), 0};
+        s.nw = std::max(0, std::min(s.R, p.nw - r0));
+        e = pick_var(p.K, s.R)(p, s, (const VarObj *)w->d, (uint32_t)nobj, (uint32_t)total, d_bad, st);
+    }
+    if (e == hipSuccess) e = hipEventRecord(w->done, st);
     return e;
 }
 

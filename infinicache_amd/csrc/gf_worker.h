@@ -1,0 +1,68 @@
+// gf_worker.h — the resident per-object coder (rsgpu_worker_start,
+// include/rsgpu.h): shared host/device layout of its mailboxes and its
+// launch arguments.
+//
+// The reference codes ONE object per EcSet / EcGet call (client/ecRedis.go:96,
+// :173; its example object is 1 KiB, client/example/main.go:15,26).  On the
+// stream path every such call pays a kernel launch and a stream
+// synchronisation (>= 10.8 us for an empty kernel on MI355X,
+// profiles/r03_mailbox_probe_hostpoll.txt), more than the coding itself.  The
+// worker is one launch of `nslots` workgroups that stay resident: workgroup w
+// polls mailbox w in coherent pinned host memory, codes the object the
+// request names (reading its rows from, and writing them to, pinned host
+// memory over PCIe) and publishes a response word the caller spins on.
+//
+// Request: one 64-B line of eight 8-B granules {payload, tag}.  The caller
+// writes every granule with one 8-B store, tag = the slot's next request
+// number; the worker accepts the line only when all eight tags carry that
+// number, so a read that raced the caller's stores is simply polled again.
+#pragma once
+#include <cstdint>
+
+namespace rsgpu {
+
+enum WorkerOp : uint32_t {
+    kWopEncode = 0,        // Encode: parity rows <- M[k:] x data rows
+    kWopEncodeVerify = 1,  // Encode, then Verify on the parity rows as stored (read back)
+    kWopVerify = 2,        // Verify: check rows over all n rows
+    kWopReconstruct = 3,   // atlas mode kAtlasReconstruct
+    kWopReconstructData = 4,
+    kWopDecode = 5,        // fused Client.decode (atlas mode kAtlasDecode)
+};
+
+// granule payloads of a request line
+enum WorkerField { kWfOp = 0, kWfShardLen = 1, kWfMask = 2, kWfPitch = 3, kWfInLo = 4, kWfInHi = 5, kWfOutLo = 6,
+                   kWfOutHi = 7 };
+
+struct alignas(64) WorkerReq {
+    uint64_t g[8];  // low 32 bits: payload (WorkerField), high 32 bits: tag (request number)
+};
+struct alignas(64) WorkerResp {
+    uint64_t done;    // low: last request number served, high: its status (0 ok, 1 mismatch)
+    uint32_t exited;  // the launch generation whose workgroup left this slot
+    uint32_t pad[13];
+};
+struct alignas(64) WorkerSlot {
+    WorkerReq req;
+    WorkerResp resp;
+};
+static_assert(sizeof(WorkerSlot) == 128, "one line per direction");
+
+constexpr uint32_t kWorkerMaxN = 16;  // codes of <= 16 shards (PatRec records)
+
+struct WorkerArgs {
+    WorkerSlot *slots;          // device view of the host mailboxes
+    const int32_t *pat[3];      // atlases by mode (kAtlasReconstruct, kAtlasData, kAtlasDecode)
+    const void *recs[3];        // PatRec [slot][nsub]
+    uint32_t nsub[3];
+    const void *enc_rec;        // Encode's records [enc_nsub]
+    const void *ver_rec;        // Verify's records [ver_nsub]
+    uint32_t enc_nsub, ver_nsub;
+    const uint32_t *ctab;       // [256][kCtabStride] coefficient tables
+    uint64_t *activity;         // device words: [0] last time any workgroup served a request, [1] closing
+    uint64_t idle_ticks;        // exit after this long without requests (s_memrealtime, 100 MHz)
+    uint32_t gen;               // launch generation (written to resp.exited on exit)
+    uint32_t n, nmask;
+};
+
+}  // namespace rsgpu

@@ -1,0 +1,536 @@
+// gf_worker.hip — the resident per-object coder (gf_worker.h): its kernel,
+// and the host side that starts it, posts requests and waits for them.
+//
+// Measured first with tools/mailbox_probe.hip (profiles/r03_mailbox_probe_hostpoll.txt):
+// an empty kernel launch + stream synchronisation costs 10.8 us p50; a
+// resident workgroup that polls a host word, reads a 1 KiB object's 10 rows
+// over PCIe, writes 2 rows back and publishes a flag answers in 7.5 us.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "ctx.h"
+#include "gf_device.h"
+#include "gf_masked.h"
+#include "gf_worker.h"
+
+namespace rsgpu {
+
+// sc0 | sc1: system-coherent buffer loads and stores (pinned host memory over
+// PCIe; the loads miss in the GPU caches, so a request re-reading a buffer
+// the host has rewritten sees the new bytes — tested in test_gpu_worker.py)
+constexpr int kSysAux = 1 | 16;
+
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Every value that steers a loop or a branch is wave-uniform (readfirstlane):
+// a divergent `if (t == 0) poll` let the compiler's structurizer run lanes
+// 1-63 of wave 0 around the request loop forever while lane 0 waited to
+// poll (tools/mailbox_probe.hip, first version: a kernel that never ended).
+__global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
+    __shared__ u32x4 lt[256][2];  // coefficient c: words 0-3, word 4 (gf_apply_lanes' layout)
+    __shared__ uint32_t sreq[8];
+    __shared__ uint32_t sexit;
+    const uint32_t t = threadIdx.x;
+    {
+        const u32x4 *ct = (const u32x4 *)(a.ctab + t * kCtabStride);
+        lt[t][0] = ct[0];
+        lt[t][1] = ct[1];
+    }
+    WorkerSlot *ms = a.slots + blockIdx.x;
+    // the last request served on this slot (by this or an earlier launch)
+    uint32_t last = rfl((uint32_t)__hip_atomic_load(&ms->resp.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    for (;;) {
+        const uint32_t want = last + 1;
+        if (t < 64) {  // wave 0 polls, all of it (wave-uniform loop)
+            uint32_t polls = 0, leave = 0;
+            for (;;) {
+                uint64_t gv = 0;
+                if (t < 8) gv = __hip_atomic_load(&ms->req.g[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const bool ok = t >= 8 || (uint32_t)(gv >> 32) == want;
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0) {  // all eight granules carry the number
+                    if (t < 8) sreq[t] = (uint32_t)gv;
+                    break;
+                }
+                if ((++polls & 63u) == 0) {
+                    // the launch closes as a whole: once one workgroup found
+                    // every slot idle for idle_ticks it raises `closing`, and
+                    // the others follow within a few polls (a caller whose
+                    // slot was left waits for the whole launch to end)
+                    if (rfl((uint32_t)__hip_atomic_load(a.activity + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                        leave = 1;
+                        break;
+                    }
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    uint64_t act = __hip_atomic_load(a.activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    act = rfl((uint32_t)act) | ((uint64_t)rfl((uint32_t)(act >> 32)) << 32);
+                    const uint64_t ref = act > t_last ? act : t_last;
+                    if (now > ref && now - ref > a.idle_ticks) {
+                        if (t == 0) __hip_atomic_store(a.activity + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        leave = 1;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (t == 0) sexit = leave;
+        }
+        __syncthreads();
+        const uint32_t leave = rfl(sexit);
+        const uint32_t op = rfl(sreq[kWfOp]);
+        __syncthreads();  // sreq / sexit are rewritten by the next poll
+        if (leave || op > kWopDecode) {
+            // idle (or a stop request): tell the host this slot's workgroup is gone
+            if (t == 0) {
+                if (!leave) __hip_atomic_store(a.activity + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!leave) __hip_atomic_store(&ms->resp.done, (uint64_t)want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&ms->resp.exited, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return;
+        }
+        const uint32_t S = rfl(sreq[kWfShardLen]), mask = rfl(sreq[kWfMask]), pitch = rfl(sreq[kWfPitch]);
+        const uint64_t inb = (uint64_t)rfl(sreq[kWfInLo]) | ((uint64_t)rfl(sreq[kWfInHi]) << 32);
+        const uint64_t outb = (uint64_t)rfl(sreq[kWfOutLo]) | ((uint64_t)rfl(sreq[kWfOutHi]) << 32);
+
+        // the operation's records (uniform, scalar loads from device memory)
+        constant_ptr<PatRec> rec = nullptr;
+        uint32_t nsub = 0;
+        if (op <= kWopEncodeVerify) {
+            rec = (constant_ptr<PatRec>)a.enc_rec;
+            nsub = a.enc_nsub;
+        } else if (op == kWopVerify) {
+            rec = (constant_ptr<PatRec>)a.ver_rec;
+            nsub = a.ver_nsub;
+        } else {
+            const uint32_t m = op - kWopReconstruct;
+            const int32_t slot = ((constant_ptr<int32_t>)a.pat[m])[mask & a.nmask];
+            if (slot >= 0) {  // else nothing to do (the host rejected too-few / singular patterns)
+                nsub = a.nsub[m];
+                rec = (constant_ptr<PatRec>)a.recs[m] + (uint32_t)slot * nsub;
+            }
+        }
+        bool mismatch = false;
+        if (nsub) {
+            const uint32_t nvec = (S + 15) / 16, tail = S - (nvec - 1) * 16;
+            const uint32_t wlast = pitch - (nvec - 1) * 16, part = wlast < 16 ? wlast : 0u;
+            const uint32_t span = (a.n - 1) * pitch + nvec * 16;
+            const __amdgpu_buffer_rsrc_t rsi = __builtin_amdgcn_make_buffer_rsrc((void *)inb, (short)0, (int)span, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc((void *)outb, (short)0, (int)span, 0x00020000);
+            const constant_ptr<uint32_t> r0 = (constant_ptr<uint32_t>)rec;
+            const uint32_t kact = r0[0] & 0xffu;
+            const uint32_t irow[4] = {r0[20], r0[21], r0[22], r0[23]};
+            for (uint32_t c0 = 0; c0 < nvec; c0 += 256) {
+                const uint32_t v = c0 + t;
+                const bool live = v < nvec;
+                const uint32_t voff = live ? v * 16u : 0xfffffff0u;  // past every range: reads 0, stores dropped
+                u32x4 x[kWorkerMaxN];
+#pragma unroll
+                for (int c = 0; c < (int)kWorkerMaxN; ++c) {
+                    x[c] = u32x4{0u, 0u, 0u, 0u};
+                    if ((uint32_t)c < kact)
+                        x[c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, voff, ((irow[c >> 2] >> (8 * (c & 3))) & 0xffu) * pitch,
+                                                                     kSysAux);
+                }
+                for (uint32_t s = 0; s < nsub; ++s) {
+                    const constant_ptr<uint32_t> rw = (constant_ptr<uint32_t>)(rec + s);
+                    const uint32_t h0 = rw[0], orow = rw[2];
+                    const uint32_t nr = (h0 >> 8) & 0xffu, nw = (h0 >> 16) & 0xffu;
+                    uint32_t acc[4][4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+#pragma unroll
+                    for (int c = 0; c < (int)kWorkerMaxN; ++c) {
+                        if ((uint32_t)c < kact) {
+                            GfIdx g[4];
+#pragma unroll
+                            for (int d = 0; d < 4; ++d) g[d] = gf_idx(x[c][d]);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const uint32_t cf = (rw[4 + r * 4 + (c >> 2)] >> (8 * (c & 3))) & 0xffu;
+                                const u32x4 tw = lt[cf][0];
+                                const uint32_t t4 = lt[cf][1][0];
+#pragma unroll
+                                for (int d = 0; d < 4; ++d) acc[r][d] = gf_mac_w(acc[r][d], tw, t4, g[d]);
+                            }
+                        }
+                    }
+                    const uint32_t valid = v == nvec - 1 ? tail : 16u;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if ((uint32_t)r >= nr) continue;
+                        if ((uint32_t)r < nw) {
+                            const uint32_t row = (orow >> (8 * r)) & 0xffu;
+                            const u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+                            store_row<kSysAux>(o, rso, voff, row * pitch, v == nvec - 1 ? part : 0u);
+                        } else if (live) {
+#pragma unroll
+                            for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+                        }
+                    }
+                    if (op == kWopEncodeVerify && nw > 0) {
+                        // Verify on the parity rows as stored: this wave's stores
+                        // complete, then the rows read back over PCIe (a read does
+                        // not pass the posted writes before it) and compared
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            if ((uint32_t)r >= nw) continue;
+                            const uint32_t row = (orow >> (8 * r)) & 0xffu;
+                            const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rso, voff, row * pitch, kSysAux);
+                            if (live)
+#pragma unroll
+                                for (int d = 0; d < 4; ++d) mismatch |= ((b[d] ^ acc[r][d]) & tail_mask(d, valid)) != 0;
+                        }
+                    }
+                }
+            }
+        }
+        // every wave's stores complete before the response is published
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int bad = __syncthreads_or(mismatch);
+        if (t == 0) {
+            __hip_atomic_store(&ms->resp.done, (uint64_t)want | ((uint64_t)(bad ? 1u : 0u) << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.activity, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        last = want;
+        t_last = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+}  // namespace rsgpu
+
+// ============================================================ host side
+
+namespace rsgpu {
+
+struct Worker {
+    int nslots = 0;
+    size_t max_shard = 0;
+    WorkerSlot *h_slots = nullptr, *d_slots = nullptr;  // coherent pinned mailboxes
+    std::vector<uint8_t *> stage_h, stage_d;            // per slot: a coherent pinned object image
+    size_t stage_cap = 0;
+    std::vector<uint32_t> seq;                          // per slot: last request number posted
+    std::atomic<uint64_t> free_mask{0};                 // bit i: slot i free
+    hipStream_t stream = nullptr;                       // its own hardware queue (CU-mask stream)
+    uint64_t *d_state = nullptr;                        // [0] activity (realtime), [1] closing
+    void *d_enc = nullptr, *d_ver = nullptr;            // Encode / Verify records
+    uint32_t enc_nsub = 0, ver_nsub = 0;
+    AtlasView views[3];
+    uint64_t idle_ticks = 0;
+    std::mutex mu;                                      // launches
+    std::atomic<uint32_t> gen{1};                       // the launch the mailboxes belong to
+    std::atomic<uint64_t> served{0}, declined{0}, launches{0};  // rsgpu_worker_stats
+    ~Worker() {
+        if (stream) (void)hipStreamDestroy(stream);
+        if (h_slots) (void)hipHostFree(h_slots);
+        for (uint8_t *p : stage_h)
+            if (p) (void)hipHostFree(p);
+        if (d_state) (void)hipFree(d_state);
+        if (d_enc) (void)hipFree(d_enc);
+        if (d_ver) (void)hipFree(d_ver);
+    }
+};
+
+void WorkerDeleter::operator()(Worker *w) const { delete w; }
+
+namespace {
+
+// PatRec records of a plan whose inputs are rows [0, K) in index order
+// (Encode: the data rows; Verify: every row), one per sub-pass of <= 4 rows
+std::vector<PatRec> plan_records(const Plan &p) {
+    const int nsub = std::max(1, (p.R + 3) / 4);
+    std::vector<PatRec> recs(nsub);
+    std::memset(recs.data(), 0, recs.size() * sizeof(PatRec));
+    int nchk = 0;
+    for (int s = 0; s < nsub; ++s) {
+        const int nr = std::max(0, std::min(4, p.R - 4 * s)), nw = std::max(0, std::min(nr, p.nw - 4 * s));
+        nchk += nw < nr;
+    }
+    for (int s = 0; s < nsub; ++s) {
+        PatRec &rc = recs[s];
+        const int r0 = 4 * s, nr = std::max(0, std::min(4, p.R - r0)), nw = std::max(0, std::min(nr, p.nw - r0));
+        rc.kact = (uint8_t)p.K;
+        rc.nr = (uint8_t)nr;
+        rc.nw = (uint8_t)nw;
+        rc.nchk = (uint8_t)nchk;
+        for (int c = 0; c < p.K; ++c) rc.in_row[c] = (uint8_t)p.in_rows[c];
+        for (int r = 0; r < nr; ++r) {
+            if (r < nw) rc.out_row[r] = (uint8_t)p.out_rows[r0 + r];
+            for (int c = 0; c < p.K; ++c) rc.coef[r][c] = p.coef[(size_t)(r0 + r) * p.K + c];
+        }
+    }
+    return recs;
+}
+
+hipError_t upload(const std::vector<PatRec> &r, void *&d) {
+    hipError_t e = hipMalloc(&d, r.size() * sizeof(PatRec));
+    if (e == hipSuccess) e = hipMemcpy(d, r.data(), r.size() * sizeof(PatRec), hipMemcpyHostToDevice);
+    return e;
+}
+
+// launch generation `g` of the worker (w->mu held)
+hipError_t launch(Worker &w, uint32_t g) {
+    WorkerArgs a{};
+    a.slots = w.d_slots;
+    for (int m = 0; m < 3; ++m) {
+        a.pat[m] = w.views[m].pat;
+        a.recs[m] = w.views[m].recs;
+        a.nsub[m] = (uint32_t)w.views[m].nsub;
+    }
+    a.enc_rec = w.d_enc;
+    a.ver_rec = w.d_ver;
+    a.enc_nsub = w.enc_nsub;
+    a.ver_nsub = w.ver_nsub;
+    a.ctab = w.views[0].ctab;
+    a.activity = w.d_state;
+    a.idle_ticks = w.idle_ticks;
+    a.gen = g;
+    a.n = (uint32_t)w.views[0].n;
+    a.nmask = (uint32_t)((1u << w.views[0].n) - 1);
+    hipError_t e = hipMemsetAsync(w.d_state, 0, 16, w.stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(gf_worker, dim3(w.nslots), dim3(256), 0, w.stream, a);
+    return hipGetLastError();
+}
+
+int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard, std::unique_ptr<Worker> &out) {
+    std::unique_ptr<Worker> w(new Worker());
+    w->nslots = nslots;
+    w->max_shard = max_shard;
+    w->idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
+    for (int m = 0; m < 3; ++m) {
+        int e = ctx->atlas_view((AtlasMode)m, w->views[m]);
+        if (e) return e;
+    }
+    std::vector<PatRec> er = plan_records(*ctx->plan_encode()), vr = plan_records(*ctx->plan_verify());
+    w->enc_nsub = (uint32_t)er.size();
+    w->ver_nsub = (uint32_t)vr.size();
+    HIP_TRY(upload(er, w->d_enc));
+    HIP_TRY(upload(vr, w->d_ver));
+    HIP_TRY(hipMalloc(&w->d_state, 16));
+    // a CU-masked stream is its own hardware queue: no other stream's work
+    // queues behind the resident kernel
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    std::vector<uint32_t> cu_mask((size_t)(cus + 31) / 32, 0xffffffffu);
+    if (cus % 32) cu_mask.back() = (1u << (cus % 32)) - 1;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&w->stream, (uint32_t)cu_mask.size(), cu_mask.data()));
+    HIP_TRY(hipHostMalloc((void **)&w->h_slots, sizeof(WorkerSlot) * nslots, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset((void *)w->h_slots, 0, sizeof(WorkerSlot) * nslots);
+    for (int i = 0; i < nslots; ++i) w->h_slots[i].resp.exited = 1;  // generation 1: not running
+    HIP_TRY(hipHostGetDevicePointer((void **)&w->d_slots, w->h_slots, 0));
+    w->stage_cap = (size_t)ctx->n * max_shard + 64;
+    w->stage_h.assign(nslots, nullptr);
+    w->stage_d.assign(nslots, nullptr);
+    for (int i = 0; i < nslots; ++i) {
+        HIP_TRY(hipHostMalloc((void **)&w->stage_h[i], w->stage_cap, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer((void **)&w->stage_d[i], w->stage_h[i], 0));
+    }
+    w->seq.assign(nslots, 0);
+    w->free_mask.store(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
+    out = std::move(w);
+    return RSGPU_OK;
+}
+
+int acquire_slot(Worker &w) {
+    uint64_t m = w.free_mask.load(std::memory_order_relaxed);
+    while (m) {
+        const int i = __builtin_ctzll(m);
+        if (w.free_mask.compare_exchange_weak(m, m & ~(1ull << i), std::memory_order_acquire)) return i;
+    }
+    return -1;
+}
+void release_slot(Worker &w, int i) { w.free_mask.fetch_or(1ull << i, std::memory_order_release); }
+
+// Posts request `rq` (payloads) on slot i and waits for its response;
+// relaunches the resident kernel when it had left (idle) before serving it.
+int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
+    WorkerSlot &s = w.h_slots[i];
+    const uint32_t n = ++w.seq[i];
+    for (int g = 0; g < 8; ++g)
+        __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)n << 32), __ATOMIC_RELEASE);
+    uint32_t cur = w.gen.load(std::memory_order_acquire);
+    unsigned spins = 0;
+    for (;;) {
+        const uint64_t d = __atomic_load_n(&s.resp.done, __ATOMIC_ACQUIRE);
+        if ((uint32_t)d == n) {
+            status = (uint32_t)(d >> 32);
+            return RSGPU_OK;
+        }
+        if (__atomic_load_n(&s.resp.exited, __ATOMIC_ACQUIRE) == cur) {
+            // this slot's workgroup of launch `cur` is gone (idle, or never
+            // launched): the request line stays posted, a new launch serves it
+            std::lock_guard<std::mutex> l(w.mu);
+            if (w.gen.load() == cur) {
+                HIP_TRY(hipStreamSynchronize(w.stream));  // every workgroup of `cur` leaves promptly
+                HIP_TRY(launch(w, cur + 1));
+                w.gen.store(cur + 1, std::memory_order_release);
+                w.launches.fetch_add(1, std::memory_order_relaxed);
+            }
+            cur = w.gen.load(std::memory_order_acquire);
+            continue;
+        }
+        if ((++spins & 0xfffffu) == 0) {  // a kernel that died without answering
+            const hipError_t q = hipStreamQuery(w.stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "resident worker");
+        }
+    }
+}
+
+}  // namespace
+
+// The worker serves one object when it can: returns RSGPU_OK with *bad set
+// (0 / 1), kWorkerDeclined to use the stream path, or an error.
+int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *const *rows, uint32_t *bad) {
+    Worker *w = ctx->worker.get();
+    if (!w || S > w->max_shard || S == 0) return kWorkerDeclined;
+    const int n = ctx->n, k = ctx->k;
+    const uint32_t full = (1u << n) - 1;
+    // rows the op reads and writes
+    uint32_t rd, wr;
+    switch (op) {
+        case kWopEncode: case kWopEncodeVerify: rd = (1u << k) - 1; wr = full & ~rd; break;
+        case kWopVerify: rd = full; wr = 0; break;
+        case kWopReconstructData: rd = mask; wr = ~mask & ((1u << k) - 1); break;
+        default: rd = mask; wr = ~mask & full; break;
+    }
+    const int i = acquire_slot(*w);
+    if (i < 0) {  // every mailbox busy: the stream path takes this call
+        w->declined.fetch_add(1, std::memory_order_relaxed);
+        return kWorkerDeclined;
+    }
+    // one Split image in pinned memory readable past its last row's 16-B
+    // vector: the worker reads and writes it in place (zero copy)
+    bool split = true;
+    for (int r = 1; r < n && split; ++r) split = rows[r] == rows[0] + (size_t)r * S;
+    const uint8_t *img = split ? (const uint8_t *)host_device_ptr(rows[0], (size_t)(n - 1) * S + (S + 15) / 16 * 16)
+                               : nullptr;
+    if (!img) {  // stage through the slot's image
+        img = w->stage_d[i];
+        for (int r = 0; r < n; ++r)
+            if ((rd >> r) & 1) std::memcpy(w->stage_h[i] + (size_t)r * S, rows[r], S);
+    }
+    uint32_t rq[8] = {op, (uint32_t)S, mask, (uint32_t)S, (uint32_t)(uintptr_t)img,
+                      (uint32_t)((uintptr_t)img >> 32), (uint32_t)(uintptr_t)img, (uint32_t)((uintptr_t)img >> 32)};
+    uint32_t status = 0;
+    int e = post_and_wait(*w, i, rq, status);
+    if (e == RSGPU_OK && img == w->stage_d[i])
+        for (int r = 0; r < n; ++r)
+            if ((wr >> r) & 1) std::memcpy(rows[r], w->stage_h[i] + (size_t)r * S, S);
+    release_slot(*w, i);
+    if (e) return e;
+    w->served.fetch_add(1, std::memory_order_relaxed);
+    *bad = status;
+    return RSGPU_OK;
+}
+
+int worker_stop(rsgpu_ctx *ctx) {
+    Worker *w = ctx->worker.get();
+    if (!w) return RSGPU_OK;
+    // take every mailbox (calls in flight finish first), then one stop request
+    const uint64_t all = w->nslots >= 64 ? ~0ull : ((1ull << w->nslots) - 1);
+    uint64_t got = 0;
+    while (got != all) {
+        const int i = acquire_slot(*w);
+        if (i >= 0) got |= 1ull << i;
+        else std::this_thread::yield();
+    }
+    std::lock_guard<std::mutex> l(w->mu);
+    const uint32_t cur = w->gen.load();
+    if (__atomic_load_n(&w->h_slots[0].resp.exited, __ATOMIC_ACQUIRE) != cur) {
+        // running: a stop request on slot 0; its workgroup raises `closing`
+        // and every other one leaves on its next poll (the other mailboxes'
+        // request numbers stay as they are)
+        WorkerSlot &s = w->h_slots[0];
+        const uint32_t n = ++w->seq[0];
+        for (int g = 0; g < 8; ++g)
+            __atomic_store_n(&s.req.g[g], (uint64_t)(g == kWfOp ? 0xffu : 0u) | ((uint64_t)n << 32), __ATOMIC_RELEASE);
+    }
+    int e = RSGPU_OK;
+    const hipError_t he = hipStreamSynchronize(w->stream);
+    if (he != hipSuccess) e = hip_fail(he, "worker stop");
+    w->free_mask.store(all);
+    return e;
+}
+
+}  // namespace rsgpu
+
+// ============================================================== C ABI
+
+extern "C" {
+
+int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard) {
+    if (!ctx || nslots < 0 || nslots > 64) return RSGPU_ERR_INVALID_ARG;
+    if (ctx->multi()) {
+        for (auto &c : ctx->subs) {
+            const int e = rsgpu_worker_start(c.get(), nslots, idle_us, max_shard);
+            if (e) return e;
+        }
+        return RSGPU_OK;
+    }
+    if (ctx->n > (int)kWorkerMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
+    if (atlas_estimate(ctx->k, ctx->p, true) > ((size_t)32 << 20)) return RSGPU_ERR_NOT_IMPLEMENTED;
+    if (!nslots) nslots = 8;
+    if (!idle_us) idle_us = 50000;
+    if (!max_shard) max_shard = 16384;
+    if (max_shard > ((size_t)1 << 24)) return RSGPU_ERR_INVALID_ARG;
+    DeviceGuard dg_;
+    int e = ctx->use_device(dg_);
+    if (e) return e;
+    std::lock_guard<std::mutex> l(ctx->worker_mu);
+    if (ctx->worker) {  // restart with the new settings
+        if ((e = worker_stop(ctx))) return e;
+        ctx->worker.reset();
+    }
+    std::unique_ptr<Worker> w;
+    if ((e = worker_create(ctx, nslots, idle_us, max_shard, w))) return e;
+    ctx->worker.reset(w.release());
+    return RSGPU_OK;
+}
+
+int rsgpu_worker_stats(const rsgpu_ctx *ctx, uint64_t *served, uint64_t *declined, uint64_t *launches) {
+    if (!ctx) return RSGPU_ERR_INVALID_ARG;
+    uint64_t s = 0, d = 0, l = 0;
+    auto add = [&](const rsgpu_ctx *c) {
+        if (const Worker *w = c->worker.get()) {
+            s += w->served.load();
+            d += w->declined.load();
+            l += w->launches.load();
+        }
+    };
+    add(ctx);
+    for (auto &c : ctx->subs) add(c.get());
+    if (served) *served = s;
+    if (declined) *declined = d;
+    if (launches) *launches = l;
+    return RSGPU_OK;
+}
+
+int rsgpu_worker_stop(rsgpu_ctx *ctx) {
+    if (!ctx) return RSGPU_ERR_INVALID_ARG;
+    if (ctx->multi()) {
+        int first = RSGPU_OK;
+        for (auto &c : ctx->subs) {
+            const int e = rsgpu_worker_stop(c.get());
+            if (!first) first = e;
+        }
+        return first;
+    }
+    std::lock_guard<std::mutex> l(ctx->worker_mu);
+    if (!ctx->worker) return RSGPU_OK;
+    DeviceGuard dg_;
+    int e = ctx->use_device(dg_);
+    if (!e) e = worker_stop(ctx);
+    ctx->worker.reset();
+    return e;
+}
+
+}  // extern "C"

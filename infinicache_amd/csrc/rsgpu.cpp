@@ -32,6 +32,7 @@
 #include "gf256.h"
 #include "gf_apply.h"
 #include "gf_masked.h"
+#include "gf_worker.h"
 
 namespace rsgpu {
 
@@ -655,6 +656,7 @@ int rsgpu_device_calls(const rsgpu_ctx *ctx, uint64_t *out, int cap) {
 
 void rsgpu_destroy(rsgpu_ctx *ctx) {
     if (!ctx) return;
+    (void)rsgpu_worker_stop(ctx);  // the resident kernel reads this context's tables
     for (auto &c : ctx->subs) rsgpu_destroy(c.release());  // each on its own device
     DeviceGuard g;  // frees its device memory on its device, then restores the caller's
     int cur = -1;
@@ -682,6 +684,8 @@ int rsgpu_encode(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
     if (e) return e;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
+    uint32_t wbad = 0;
+    if ((e = worker_run(ctx, kWopEncode, size, 0, shards, &wbad)) != kWorkerDeclined) return e;
     auto plan = ctx->plan_encode();
     std::vector<const uint8_t *> in(shards, shards + ctx->k);
     std::vector<uint8_t *> out(shards + ctx->k, shards + ctx->n);
@@ -698,6 +702,11 @@ int rsgpu_encode_verify(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *le
     if (e) return e;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
+    uint32_t wbad = 0;
+    if ((e = worker_run(ctx, kWopEncodeVerify, size, 0, shards, &wbad)) != kWorkerDeclined) {
+        if (e == RSGPU_OK) *ok = wbad == 0;
+        return e;
+    }
     auto enc = ctx->plan_encode();
     auto ver = ctx->plan_verify();
     std::vector<const uint8_t *> in(shards, shards + ctx->k);
@@ -719,6 +728,11 @@ int rsgpu_verify(rsgpu_ctx *ctx, const uint8_t *const *shards, const size_t *len
     if (e) return e;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
+    uint32_t wbad = 0;
+    if ((e = worker_run(ctx, kWopVerify, size, 0, const_cast<uint8_t *const *>(shards), &wbad)) != kWorkerDeclined) {
+        if (e == RSGPU_OK) *ok = wbad == 0;
+        return e;
+    }
     auto plan = ctx->plan_verify();
     std::vector<const uint8_t *> in(shards, shards + ctx->n);
     uint32_t bad = 1;
@@ -749,6 +763,22 @@ static int reconstruct_common(rsgpu_ctx *ctx, uint8_t *const *shards, const size
         if (!shards[plan->out_rows[r]]) return RSGPU_ERR_INVALID_ARG;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
+    if (ctx->worker) {
+        // the worker writes every missing row it rebuilds through rows[i]:
+        // each needs a buffer (ReconstructData: the missing data rows only)
+        bool bufs = true;
+        uint32_t mask = 0;
+        for (int i = 0; i < ctx->n; ++i) {
+            mask |= (uint32_t)present[i] << i;
+            if (!present[i] && !shards[i] && (!data_only || i < ctx->k)) bufs = false;
+        }
+        uint32_t wbad = 0;
+        if (bufs && (e = worker_run(ctx, check ? kWopDecode : data_only ? kWopReconstructData : kWopReconstruct, size,
+                                    mask, shards, &wbad)) != kWorkerDeclined) {
+            if (e == RSGPU_OK && ok) *ok = wbad == 0;
+            return e;
+        }
+    }
     std::vector<const uint8_t *> in;
     for (int row : plan->in_rows) in.push_back(shards[row]);
     std::vector<uint8_t *> out;
@@ -1163,6 +1193,94 @@ int rsgpu_reconstruct_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_
                       data_only, d_status, stream)
     return dev_masks(ctx, d_base, d_masks, shard_len, pitch, obj_stride, nobj,
                      data_only ? kAtlasData : kAtlasReconstruct, d_status, stream);
+}
+
+// ---------------------------------------------- variable-size device batches
+
+static_assert(sizeof(rsgpu_dev_obj) == sizeof(DevObj) && offsetof(rsgpu_dev_obj, shard_len) == offsetof(DevObj, shard_len) &&
+                  offsetof(rsgpu_dev_obj, pitch) == offsetof(DevObj, pitch),
+              "rsgpu_dev_obj and DevObj share one layout");
+
+// Argument checks of a variable-size table; multi-device contexts: the
+// entry that owns the objects' memory (all on one device)
+static int objs_prepare(rsgpu_ctx *&ctx, const rsgpu_dev_obj *objs, int nobj) {
+    if (!ctx || nobj < 0 || (nobj > 0 && !objs)) return RSGPU_ERR_INVALID_ARG;
+    for (int o = 0; o < nobj; ++o) {
+        const rsgpu_dev_obj &d = objs[o];
+        if (!d.base) return RSGPU_ERR_INVALID_ARG;
+        if (d.shard_len == 0) return RSGPU_ERR_SHARD_NO_DATA;
+        if (d.pitch < (d.shard_len + 15) / 16 * 16) return RSGPU_ERR_INVALID_ARG;
+        if ((size_t)ctx->n * d.pitch >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
+    }
+    if (ctx->multi() && nobj > 0) {
+        rsgpu_ctx *sub = ctx->sub_for(objs[0].base);
+        if (!sub) return RSGPU_ERR_INVALID_ARG;
+        for (int o = 1; o < nobj; ++o) {
+            hipPointerAttribute_t at;
+            if (hipPointerGetAttributes(&at, objs[o].base) != hipSuccess || at.device != sub->device)
+                return RSGPU_ERR_INVALID_ARG;
+        }
+        ctx = sub;
+    }
+    return RSGPU_OK;
+}
+
+int rsgpu_encode_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, void *stream) {
+    int e = objs_prepare(ctx, objs, nobj);
+    if (e) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
+    if (nobj == 0) return RSGPU_OK;
+    auto plan = ctx->plan_encode();
+    HIP_TRY(launch_plan_objs(*plan, (const DevObj *)objs, nobj, nullptr, (hipStream_t)stream, ctx->multi_ws));
+    return RSGPU_OK;
+}
+
+int rsgpu_verify_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, uint32_t *d_bad, void *stream) {
+    if (!d_bad) return RSGPU_ERR_INVALID_ARG;
+    int e = objs_prepare(ctx, objs, nobj);
+    if (e) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
+    if (nobj == 0) return RSGPU_OK;
+    auto plan = ctx->plan_verify();
+    HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
+    HIP_TRY(launch_plan_objs(*plan, (const DevObj *)objs, nobj, d_bad, (hipStream_t)stream, ctx->multi_ws));
+    return RSGPU_OK;
+}
+
+static int recon_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, const uint8_t *present,
+                          bool data_only, bool check, uint32_t *d_bad, void *stream) {
+    if (!present || (check && !d_bad)) return RSGPU_ERR_INVALID_ARG;
+    int e = objs_prepare(ctx, objs, nobj);
+    if (e) return e;
+    int np = 0;
+    for (int i = 0; i < ctx->n; ++i) np += present[i] != 0;
+    if (np < ctx->k) return RSGPU_ERR_TOO_FEW_SHARDS;
+    if (np == ctx->n) {
+        if (!check) return RSGPU_OK;
+        return rsgpu_verify_dev_objs(ctx, objs, nobj, d_bad, stream);
+    }
+    std::shared_ptr<Plan> plan;
+    if ((e = ctx->plan_reconstruct(present, data_only, check, plan))) return e;
+    DeviceGuard dg_;
+    if ((e = ctx->use_device(dg_))) return e;
+    if (nobj == 0) return RSGPU_OK;
+    if (check && plan->nw < plan->R)  // check rows OR into the flags; else the pass clears them
+        HIP_TRY(hipMemsetAsync(d_bad, 0, (size_t)nobj * 4, (hipStream_t)stream));
+    HIP_TRY(launch_plan_objs(*plan, (const DevObj *)objs, nobj, check ? d_bad : nullptr, (hipStream_t)stream,
+                             ctx->multi_ws));
+    return RSGPU_OK;
+}
+
+int rsgpu_reconstruct_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, const uint8_t *present,
+                               int data_only, void *stream) {
+    return recon_dev_objs(ctx, objs, nobj, present, data_only != 0, false, nullptr, stream);
+}
+
+int rsgpu_decode_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, const uint8_t *present,
+                          uint32_t *d_bad, void *stream) {
+    return recon_dev_objs(ctx, objs, nobj, present, false, true, d_bad, stream);
 }
 
 int rsgpu_reconstruct_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_t shard_len,

@@ -226,6 +226,20 @@ class RSEncoder:
         self._L.rsgpu_devices(self._ctx, out, n)
         return list(out[:n])
 
+    def worker_start(self, nslots: int = 0, idle_us: int = 0, max_shard: int = 0) -> None:
+        """Per-object calls through the resident worker (rsgpu_worker_start):
+        no kernel launch or stream synchronisation per call."""
+        _check(self._L.rsgpu_worker_start(self._ctx, nslots, idle_us, max_shard))
+
+    def worker_stop(self) -> None:
+        _check(self._L.rsgpu_worker_stop(self._ctx))
+
+    def worker_stats(self) -> dict:
+        """{'served', 'declined', 'launches'} of the resident worker."""
+        v = [ctypes.c_uint64() for _ in range(3)]
+        _check(self._L.rsgpu_worker_stats(self._ctx, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("served", "declined", "launches"), (x.value for x in v)))
+
     def device_calls(self) -> List[int]:
         """Compute calls each entry of devices() has run (how work spread)."""
         n = self._L.rsgpu_device_calls(self._ctx, None, 0)
@@ -343,6 +357,37 @@ class RSEncoder:
         _check(self._L.rsgpu_decode_dev(self._ctx, _dptr(base), pr, shard_len, pitch, obj_stride,
                                         nobj, _dptr(bad), _stream_handle(stream)))
 
+
+    # -- variable-size device batches: objs = [(base, shard_len, pitch), ...]
+    @staticmethod
+    def _obj_table(objs):
+        t = (_lib.DevObj * max(1, len(objs)))()
+        for i, (b, s, p) in enumerate(objs):
+            t[i].base = _dptr(b)
+            t[i].shard_len = s
+            t[i].pitch = p
+        return t
+
+    def encode_dev_objs(self, objs, stream=None):
+        t = self._obj_table(objs)
+        _check(self._L.rsgpu_encode_dev_objs(self._ctx, ctypes.addressof(t), len(objs), _stream_handle(stream)))
+
+    def verify_dev_objs(self, objs, bad, stream=None):
+        t = self._obj_table(objs)
+        _check(self._L.rsgpu_verify_dev_objs(self._ctx, ctypes.addressof(t), len(objs), _dptr(bad),
+                                             _stream_handle(stream)))
+
+    def reconstruct_dev_objs(self, objs, present, data_only=False, stream=None):
+        t = self._obj_table(objs)
+        pr = (ctypes.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
+        _check(self._L.rsgpu_reconstruct_dev_objs(self._ctx, ctypes.addressof(t), len(objs), pr, int(data_only),
+                                                  _stream_handle(stream)))
+
+    def decode_dev_objs(self, objs, present, bad, stream=None):
+        t = self._obj_table(objs)
+        pr = (ctypes.c_uint8 * self.Shards)(*[1 if x else 0 for x in present])
+        _check(self._L.rsgpu_decode_dev_objs(self._ctx, ctypes.addressof(t), len(objs), pr, _dptr(bad),
+                                             _stream_handle(stream)))
 
     def _present_matrix(self, present, nobj):
         pm = np.ascontiguousarray(np.asarray(present, dtype=np.uint8).reshape(nobj, self.Shards))

@@ -208,3 +208,19 @@ def test_noncontiguous_output_buffer_rejected():
     sh = [s if i >= 4 else s[:16] for i, s in enumerate(sh)]
     with pytest.raises(ia.InvalidArgument):
         enc.Encode(sh)
+
+
+def test_dev_objs_argument_checks():
+    """rsgpu_*_dev_objs validate the whole table before any device work (no
+    device needed): NULL base, zero shard_len, a pitch below roundup16(S)."""
+    enc = ia.New(10, 2)
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev_objs([(0x1000, 100, 112), (0, 100, 112)])
+    with pytest.raises(ia.ErrShardNoData):
+        enc.encode_dev_objs([(0x1000, 0, 112)])
+    with pytest.raises(ia.InvalidArgument):
+        enc.encode_dev_objs([(0x1000, 100, 104)])  # pitch < roundup16(100)
+    with pytest.raises(ia.ErrTooFewShards):
+        enc.decode_dev_objs([(0x1000, 100, 112)], [0, 0, 0] + [1] * 9, 0x2000)
+    with pytest.raises(ia.InvalidArgument):
+        enc.decode_dev_objs([(0x1000, 100, 112)], [1] * 12, 0)  # no flag array

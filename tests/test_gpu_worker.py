@@ -1,0 +1,237 @@
+"""The resident per-object worker (rsgpu_worker_start) against the oracle,
+bit-exact: Client.encode (ecRedis.go:382-402) and Client.decode (:404-432) on
+single objects, the reference's own call granularity (one object per EcSet /
+EcGet; the example object is 1 KiB, client/example/main.go:15,26).
+
+Covered: every per-object operation (Encode, fused Encode+Verify, Verify,
+Reconstruct, ReconstructData, fused decode with real extra-shard checks),
+pinned Split images read and written in place and pageable buffers staged
+through the mailbox images, one pinned buffer rewritten between calls (the
+worker must never see stale bytes), shard sizes 1 B - 16 KiB around the
+16-B vector tails, several codes (two sub-passes for p > 4, n = 16), idle
+exit + relaunch, stop / restart, concurrent callers (declined calls take
+the stream path), objects above max_shard, and a multi-entry context."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import infinicache_amd as ia
+import oracle
+from oracle import rs_numpy as rn
+
+pytestmark = pytest.mark.gpu
+SEED = 0x3C3C
+
+
+def _full(k, p, size, idx):
+    d = rn.splitmix64_bytes(SEED, idx, k * size).reshape(k, size)
+    e, sh = oracle.encode(k, p, [d[i] for i in range(k)] + [bytes(size)] * p)
+    assert e == 0
+    return [np.frombuffer(bytes(s), np.uint8) for s in sh]
+
+
+def _image(n, S, pinned):
+    buf = ia.host_alloc(n * S) if pinned else np.zeros(n * S, np.uint8)
+    return buf, [buf[i * S:(i + 1) * S] for i in range(n)]
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_worker_every_op_vs_oracle(gpu, pinned):
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start()
+    for idx, S in enumerate([1, 15, 16, 17, 103, 410, 1000, 4096, 4099, 16384]):
+        full = _full(k, p, S, idx)
+        buf, sh = _image(n, S, pinned)
+        for j in range(k):
+            sh[j][:] = full[j]
+        assert enc.EncodeVerify(sh)
+        for j in range(n):
+            assert np.array_equal(sh[j], full[j]), (S, j)
+        sh[k][:] = 0
+        enc.Encode(sh)
+        assert np.array_equal(sh[k], full[k])
+        assert enc.Verify(sh)
+        sh[n - 1][S - 1] ^= 0x80
+        assert not enc.Verify(sh)
+        sh[n - 1][S - 1] ^= 0x80
+        # a Get that received exactly k bodies: data 0 and 5 missing (the
+        # mirror allocates their buffers, as upstream reconstruct does)
+        got = [None if j in (0, 5) else sh[j] for j in range(n)]
+        assert enc.DecodeVerify(got)
+        assert np.array_equal(got[0], full[0]) and np.array_equal(got[5], full[5])
+        # one lost data row: the extra parity shard is really checked
+        bad = [None if j == 3 else sh[j] for j in range(n)]
+        assert enc.DecodeVerify(bad)
+        assert np.array_equal(bad[3], full[3])
+        sh[11][0] ^= 1
+        bad = [None if j == 3 else sh[j] for j in range(n)]
+        assert not enc.DecodeVerify(bad)
+        assert np.array_equal(bad[3], full[3])  # rebuilt from the first k present, as upstream
+        sh[11][0] ^= 1
+        # Reconstruct / ReconstructData
+        got = [None if j in (1, 10) else sh[j] for j in range(n)]
+        enc.Reconstruct(got)
+        assert np.array_equal(got[1], full[1]) and np.array_equal(got[10], full[10])
+        got = [None if j in (2, 11) else sh[j] for j in range(n)]
+        enc.ReconstructData(got)
+        assert np.array_equal(got[2], full[2]) and got[11] is None  # parity left missing
+    st = enc.worker_stats()
+    assert st["served"] >= 80 and st["launches"] >= 1, st
+
+
+def test_worker_in_place_pinned_image_missing_rows(gpu):
+    """The Go shim's route (i): one pinned Split image, the missing rows
+    passed as their own (zero-length marked) slices of it, rebuilt in place."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start()
+    L = ia._lib.load()
+    import ctypes
+    for idx, S in enumerate([103, 2048, 5003]):
+        full = _full(k, p, S, 50 + idx)
+        buf, sh = _image(n, S, True)
+        for j in range(n):
+            sh[j][:] = full[j]
+            if j in (0, 5):
+                sh[j][:] = 0xEE
+        ok = ctypes.c_int(-1)
+        present = sum(1 << j for j in range(n) if j not in (0, 5))
+        assert L.rsgpu_decode_image(enc._ctx, buf.ctypes.data, S, n, present, ctypes.byref(ok)) == 0
+        assert ok.value == 1
+        for j in range(n):
+            assert np.array_equal(sh[j], full[j]), (S, j)
+    assert enc.worker_stats()["served"] >= 3
+
+
+def test_worker_buffer_rewritten_between_calls(gpu):
+    """One pinned image re-filled with new bytes 300 times: every request must
+    read what the host wrote last (no stale GPU cache lines)."""
+    k, p, S = 10, 2, 103
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start(nslots=2)
+    m = enc.matrix()
+    buf, sh = _image(n, S, True)
+    rng = np.random.default_rng(1)
+    for it in range(300):
+        data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        for j in range(k):
+            sh[j][:] = data[j]
+        assert enc.EncodeVerify(sh)
+        want = oracle.apply(m[k:], [data[j] for j in range(k)])
+        for r in range(p):
+            assert np.array_equal(sh[k + r], want[r]), it
+    assert enc.worker_stats()["served"] >= 300
+
+
+@pytest.mark.parametrize("k,p", [(1, 1), (4, 2), (10, 4), (6, 6), (12, 4), (13, 3)])
+def test_worker_codes(gpu, k, p):
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start()
+    rng = np.random.default_rng(n * 7 + p)
+    for it, S in enumerate([7, 333, 3000]):
+        full = _full(k, p, S, 100 + it)
+        sh = [full[j].copy() if j < k else np.zeros(S, np.uint8) for j in range(n)]
+        assert enc.EncodeVerify(sh)
+        for j in range(n):
+            assert np.array_equal(sh[j], full[j])
+        lost = sorted(rng.choice(n, int(rng.integers(1, p + 1)), replace=False).tolist())
+        got = [None if j in lost else sh[j].copy() for j in range(n)]
+        assert enc.DecodeVerify(got)
+        for j in range(n):
+            assert np.array_equal(got[j], full[j]), (k, p, S, lost, j)
+    assert enc.worker_stats()["served"] >= 6
+
+
+def test_worker_idle_exit_relaunch_and_stop(gpu):
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start(nslots=4, idle_us=2000)  # leaves after 2 ms without requests
+    full = _full(k, p, 1000, 7)
+    for rnd in range(4):
+        sh = [full[j].copy() if j < k else np.zeros(1000, np.uint8) for j in range(n)]
+        assert enc.EncodeVerify(sh)
+        assert np.array_equal(sh[k], full[k])
+        time.sleep(0.03)
+    st = enc.worker_stats()
+    assert st["launches"] >= 4, st  # one relaunch per idle period
+    enc.worker_stop()
+    served = enc.worker_stats()["served"]
+    sh = [full[j].copy() if j < k else np.zeros(1000, np.uint8) for j in range(n)]
+    assert enc.EncodeVerify(sh)  # stream path again
+    assert np.array_equal(sh[k + 1], full[k + 1])
+    enc.worker_start(nslots=3)
+    assert enc.EncodeVerify(sh)
+    assert enc.worker_stats()["served"] >= 1
+
+
+def test_worker_large_shards_take_stream_path(gpu):
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start(max_shard=4096)
+    full = _full(k, p, 9000, 9)
+    sh = [full[j].copy() if j < k else np.zeros(9000, np.uint8) for j in range(n)]
+    assert enc.EncodeVerify(sh)
+    assert np.array_equal(sh[k], full[k])
+    assert enc.worker_stats()["served"] == 0
+
+
+def test_worker_concurrent_callers(gpu):
+    """8 threads on 3 mailboxes: calls that find every mailbox busy take the
+    stream path; every result is exact either way."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start(nslots=3)
+    errors = []
+
+    def caller(tid):
+        try:
+            for i in range(25):
+                S = 64 + 37 * tid + i
+                full = _full(k, p, S, 1000 + tid * 100 + i)
+                buf, sh = _image(n, S, tid % 2 == 0)
+                for j in range(k):
+                    sh[j][:] = full[j]
+                assert enc.EncodeVerify(sh)
+                got = [None if j in (tid % n, (i + 3) % n) else sh[j] for j in range(n)]
+                assert enc.DecodeVerify(got)
+                for j in range(n):
+                    assert np.array_equal(got[j], full[j])
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=caller, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(180)
+    assert not errors, errors[:3]
+    st = enc.worker_stats()
+    assert st["served"] + st["declined"] == 8 * 25 * 2, st
+    assert st["served"] > 0
+
+
+def test_worker_multi_entry_context(gpu):
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p, devices=[0, 0])
+    enc.worker_start(nslots=2)
+    for i, S in enumerate([5, 800, 4096]):
+        full = _full(k, p, S, 300 + i)
+        sh = [full[j].copy() if j < k else np.zeros(S, np.uint8) for j in range(n)]
+        assert enc.EncodeVerify(sh)
+        got = [None if j in (i, i + 6) else sh[j] for j in range(n)]
+        assert enc.DecodeVerify(got)
+        for j in range(n):
+            assert np.array_equal(got[j], full[j])
+    assert enc.worker_stats()["served"] >= 6
+    assert all(c > 0 for c in enc.device_calls())

@@ -5,7 +5,10 @@
  * LAT_BYTES bytes (default 1 MiB; client/example/main.go uses 1 KiB), shards
  * as Split lays them out (one contiguous buffer).
  *
- *   [LAT_BYTES=N] ./lat_bench [iters [concurrent_seconds]]
+ *   [LAT_BYTES=N] [LAT_WORKER=nslots] ./lat_bench [iters [concurrent_seconds]]
+ *
+ * LAT_WORKER=nslots: the per-object calls go through the resident worker
+ * (rsgpu_worker_start with nslots mailboxes) instead of the stream path.
  *
  * Prints p50/p99 in microseconds for pageable (malloc) and pinned
  * (rsgpu_host_alloc) buffers.  No Python in the process. */
@@ -105,6 +108,12 @@ int main(int argc, char **argv) {
     rsgpu_ctx *ctx;
     printf("object %zu B (S = %zu)\n", nb, S);
     if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
+    const char *wenv = getenv("LAT_WORKER");
+    if (wenv && atoi(wenv) > 0) {
+        const int e = rsgpu_worker_start(ctx, atoi(wenv), 0, S > 16384 ? S : 0);
+        printf("resident worker: %d mailboxes (rc %d)\n", atoi(wenv), e);
+        if (e) return 1;
+    }
     double *te = malloc(sizeof(double) * iters), *td = malloc(sizeof(double) * iters);
     double *tf = malloc(sizeof(double) * iters);
     for (int pinned = 0; pinned < 2; ++pinned) {

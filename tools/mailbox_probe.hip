@@ -58,32 +58,42 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p) {
 }
 
 // VARIANT 0: release store of the flag; 1: write-through rows + vmcnt(0) + relaxed flag
+// Control flow that decides the loop must be wave-UNIFORM: with a divergent
+// `if (t == 0) poll` the compiler's structurizer let lanes 1-63 of wave 0
+// run the request loop again and again (barrier to barrier) while lane 0
+// waited to poll: a kernel that never ends.  So the whole of wave 0 polls,
+// every polled value goes through readfirstlane (scalar), and the request
+// number reaches the other waves through LDS + readfirstlane.
 template <int VARIANT, int SLEEP>
 __global__ __launch_bounds__(256) void worker(Mailbox *mb, uint32_t *bell, uint64_t idle_ticks) {
     __shared__ uint32_t s_seq;
     const uint32_t t = threadIdx.x;
     uint32_t last = 0;
+    if (t == 0) __hip_atomic_store(&mb->pad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // started
     for (;;) {
-        if (t == 0) {
-            uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        if (t < 64) {  // wave 0, all lanes: uniform loop
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             uint32_t s;
             for (;;) {
-                s = ld_sys(bell);
+                s = __builtin_amdgcn_readfirstlane(ld_sys(bell));
                 if (s != last) break;
-                if (ld_sys(&mb->stop)) { s = 0xffffffffu; break; }
+                if (__builtin_amdgcn_readfirstlane(ld_sys(&mb->stop))) { s = 0xffffffffu; break; }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) { s = 0xffffffffu; break; }
                 if (SLEEP) __builtin_amdgcn_s_sleep(SLEEP);
             }
-            s_seq = s;
+            if (t == 0) s_seq = s;
         }
         __syncthreads();
-        const uint32_t s = s_seq;
+        const uint32_t s = __builtin_amdgcn_readfirstlane(s_seq);
         __syncthreads();
         if (s == 0xffffffffu) return;
         last = s;
-        const uint32_t S = ld_sys(&mb->S);
-        const uint8_t *in = (const uint8_t *)ld_sys64(&mb->in);
-        uint8_t *out = (uint8_t *)ld_sys64(&mb->out);
+        const uint32_t S = __builtin_amdgcn_readfirstlane(ld_sys(&mb->S));
+        const uint64_t inp = ld_sys64(&mb->in), outp = ld_sys64(&mb->out);
+        const uint8_t *in = (const uint8_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(inp >> 32)) << 32) |
+                                              __builtin_amdgcn_readfirstlane((uint32_t)inp));
+        uint8_t *out = (uint8_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(outp >> 32)) << 32) |
+                                   __builtin_amdgcn_readfirstlane((uint32_t)outp));
         const uint32_t nvec = (S + 15) / 16;
         const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)(12 * S + 64), 0x00020000);
         const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)(2 * nvec * 16), 0x00020000);
@@ -163,6 +173,7 @@ static void run_poll(const char *name, bool devbell, int iters) {
     mb->out = (uint64_t)dout;
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    std::printf("%s: launching\n", name);
     hipLaunchKernelGGL((worker<VARIANT, SLEEP>), dim3(1), dim3(256), 0, st, dmb, bell_dev, (uint64_t)200000000);  // 2 s idle
     CK(hipGetLastError());
     std::vector<double> lat;
@@ -183,7 +194,8 @@ static void run_poll(const char *name, bool devbell, int iters) {
         __atomic_store_n(bell_host, (uint32_t)it, __ATOMIC_RELEASE);
         while (__atomic_load_n(&mb->resp, __ATOMIC_ACQUIRE) != (uint32_t)it) {
             if (now_us() - t0 > 1e6) {
-                std::printf("%s: no response after 1 s at request %d\n", name, it);
+                std::printf("%s: no response after 1 s at request %d (kernel started: %u)\n", name, it,
+                            __atomic_load_n(&mb->pad, __ATOMIC_ACQUIRE));
                 mb->stop = 1;
                 CK(hipStreamSynchronize(st));
                 return;
@@ -193,7 +205,8 @@ static void run_poll(const char *name, bool devbell, int iters) {
         if (std::memcmp(out, want[0], S) || std::memcmp(out + 112, want[1], S)) ++bad;
         lat.push_back(t1 - t0);
     }
-    mb->stop = 1;
+    __atomic_store_n(&mb->stop, 1u, __ATOMIC_RELEASE);
+    std::printf("%s: stop sent, waiting for the kernel\n", name);
     CK(hipStreamSynchronize(st));
     std::printf("%-34s p50 %6.2f us  p90 %6.2f  p99 %6.2f  min %6.2f  (%d iters, %d wrong)\n", name, pct(lat, 0.5),
                 pct(lat, 0.9), pct(lat, 0.99), pct(lat, 0.0), iters, bad);
@@ -205,7 +218,9 @@ static void run_poll(const char *name, bool devbell, int iters) {
 }
 
 int main(int argc, char **argv) {
+    setvbuf(stdout, nullptr, _IONBF, 0);
     const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+    const int only = argc > 2 ? std::atoi(argv[2]) : -1;  // run one variant
     CK(hipSetDevice(0));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -220,10 +235,10 @@ int main(int argc, char **argv) {
         std::printf("%-34s p50 %6.2f us  p90 %6.2f  p99 %6.2f  min %6.2f\n", "launch+sync (empty kernel)",
                     pct(lat, 0.5), pct(lat, 0.9), pct(lat, 0.99), pct(lat, 0.0));
     }
-    run_poll<0, 1>("hostpoll release-flag sleep1", false, iters);
-    run_poll<1, 1>("hostpoll wt-rows+flag sleep1", false, iters);
-    run_poll<1, 0>("hostpoll wt-rows+flag nosleep", false, iters);
-    run_poll<1, 4>("hostpoll wt-rows+flag sleep4", false, iters);
-    run_poll<1, 1>("devpoll wt-rows+flag sleep1", true, iters);
+    if (only < 0 || only == 0) run_poll<0, 1>("hostpoll release-flag sleep1", false, iters);
+    if (only < 0 || only == 1) run_poll<1, 1>("hostpoll wt-rows+flag sleep1", false, iters);
+    if (only < 0 || only == 2) run_poll<1, 0>("hostpoll wt-rows+flag nosleep", false, iters);
+    if (only < 0 || only == 3) run_poll<1, 4>("hostpoll wt-rows+flag sleep4", false, iters);
+    if (only == 4) run_poll<1, 1>("devpoll wt-rows+flag sleep1", true, iters);
     return 0;
 }
