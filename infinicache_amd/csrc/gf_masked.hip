@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "gf_apply.h"
 #include "gf_launch.h"
@@ -33,6 +34,12 @@ hipError_t launch_masked_t(const AtlasView &A, const Layout &L, const uint32_t *
     a.nobj = (uint32_t)L.nobj;
     // occupancy cap for the common pattern (a healthy Get: k inputs, rows written)
     const unsigned cap = store_lds(A.kcap);
+    // tuning knob (measurement only): workgroups per CU of the lanes kernel
+    static const int lanes_w = [] {
+        const char *e = std::getenv("RSGPU_LANES_WG");
+        return e ? std::atoi(e) : 0;
+    }();
+    const unsigned lanes_cap = lanes_w > 0 ? 160u * 1024u / (unsigned)lanes_w - 256u : cap;
     // Short rows: a workgroup codes opw whole objects (gf_apply_lanes), all
     // lanes addressing them from the group's first object in one 32-bit range
     uint32_t opw = 1;
@@ -46,7 +53,7 @@ hipError_t launch_masked_t(const AtlasView &A, const Layout &L, const uint32_t *
             a.opw = opw;
             a.gspan = (uint32_t)((uint64_t)(opw - 1) * L.obj_stride + a.span);
             constexpr unsigned stat = sizeof(u32x4) * 256 * 2 + 4 * 256;  // gf_apply_lanes' static LDS
-            const unsigned dyn = cap > stat ? cap - stat : 0u;
+            const unsigned dyn = lanes_cap > stat ? lanes_cap - stat : 0u;
             const size_t groups = ((size_t)L.nobj + opw - 1) / opw;
             for (size_t g0 = 0; g0 < groups; g0 += (size_t)max_items(1)) {
                 const size_t ng = std::min((size_t)max_items(1), groups - g0);

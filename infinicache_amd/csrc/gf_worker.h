@@ -54,15 +54,18 @@ struct WorkerArgs {
     WorkerSlot *slots;          // device view of the host mailboxes
     const int32_t *pat[3];      // atlases by mode (kAtlasReconstruct, kAtlasData, kAtlasDecode)
     const void *recs[3];        // PatRec [slot][nsub]
-    uint32_t nsub[3];
+    const uint32_t *tabs[3];    // [slot][nsub][tk][tr][kTabWords] v_perm tables
+    uint32_t nsub[3], tk[3], tr[3];
     const void *enc_rec;        // Encode's records [enc_nsub]
     const void *ver_rec;        // Verify's records [ver_nsub]
-    uint32_t enc_nsub, ver_nsub;
-    const uint32_t *ctab;       // [256][kCtabStride] coefficient tables
+    const uint32_t *enc_tab, *ver_tab;  // their tables [nsub][k or n][enc_r / ver_r][kTabWords]
+    uint32_t enc_nsub, ver_nsub, enc_r, ver_r;
+    const uint32_t *ctab;       // [256][kCtabStride] coefficient tables (unused by the kernel)
     uint64_t *activity;         // device words: [0] last time any workgroup served a request, [1] closing
     uint64_t idle_ticks;        // exit after this long without requests (s_memrealtime, 100 MHz)
     uint32_t gen;               // launch generation (written to resp.exited on exit)
-    uint32_t n, nmask;
+    uint32_t n, nmask, k;
+    uint32_t trace;             // write device stamps into resp.pad (RSGPU_WORKER_TRACE)
 };
 
 }  // namespace rsgpu

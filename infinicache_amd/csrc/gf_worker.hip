@@ -30,11 +30,39 @@ __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_re
 // a divergent `if (t == 0) poll` let the compiler's structurizer run lanes
 // 1-63 of wave 0 around the request loop forever while lane 0 waited to
 // poll (tools/mailbox_probe.hip, first version: a kernel that never ended).
+//
+// Latency path of one request (RSGPU_WORKER_TRACE):
+//   * all four waves poll the request line, staggered, so a poll read is
+//     always in flight;
+//   * the input rows follow from the operation and the present mask alone
+//     (the first k present rows, upstream's survivor rule; the fused decode
+//     also reads the extras its check rows compare), so the data loads go out
+//     before the atlas lookup of the pattern's record, which overlaps them;
+//   * small objects are coded lane-parallel: lane = (input, vector), each
+//     lane multiplies ONE input vector into every row and the partial rows
+//     are XOR-reduced through LDS.  The first form (lane = vector, every
+//     input and row in one lane) kept 7 lanes of one wave busy for a 1 KiB
+//     object and spent 3.9 us in dependent table lookups and VALU work after
+//     the data had arrived;
+//   * larger objects (more vectors than the lanes hold) go lane = vector,
+//     256 vectors per chunk.
+constexpr uint32_t kLaneVecs = 64;  // lane-parallel path: vectors per pass at most
+constexpr uint32_t kLaneU = 4;      // ... and passes (their loads issued up front)
+
+// the c-th set bit of m (per lane; m < 2^16)
+__device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t c) {
+#pragma unroll
+    for (uint32_t i = 0; i < kWorkerMaxN; ++i) m = i < c ? (m & (m - 1u)) : m;
+    return m ? (uint32_t)__builtin_ctz(m) : 0u;
+}
+
+template <int RM>
 __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
-    __shared__ u32x4 lt[256][2];  // coefficient c: words 0-3, word 4 (gf_apply_lanes' layout)
+    __shared__ u32x4 lt[256][2];                 // coefficient c: words 0-3, word 4 (gf_apply_lanes' layout)
+    __shared__ u32x4 red[RM][kWorkerMaxN][kLaneVecs];  // lane-parallel partial rows
     __shared__ uint32_t sreq[8];
-    __shared__ uint32_t sexit;
-    const uint32_t t = threadIdx.x;
+    __shared__ uint32_t sfound;   // the request number a poll found, or ~0u: leave
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     {
         const u32x4 *ct = (const u32x4 *)(a.ctab + t * kCtabStride);
         lt[t][0] = ct[0];
@@ -44,58 +72,125 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
     // the last request served on this slot (by this or an earlier launch)
     uint32_t last = rfl((uint32_t)__hip_atomic_load(&ms->resp.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    if (t == 0) sfound = last;
     __syncthreads();
     for (;;) {
         const uint32_t want = last + 1;
-        if (t < 64) {  // wave 0 polls, all of it (wave-uniform loop)
-            uint32_t polls = 0, leave = 0;
-            for (;;) {
-                uint64_t gv = 0;
-                if (t < 8) gv = __hip_atomic_load(&ms->req.g[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const bool ok = t >= 8 || (uint32_t)(gv >> 32) == want;
-                if (__builtin_amdgcn_ballot_w64(!ok) == 0) {  // all eight granules carry the number
-                    if (t < 8) sreq[t] = (uint32_t)gv;
-                    break;
-                }
-                if ((++polls & 63u) == 0) {
-                    // the launch closes as a whole: once one workgroup found
-                    // every slot idle for idle_ticks it raises `closing`, and
-                    // the others follow within a few polls (a caller whose
-                    // slot was left waits for the whole launch to end)
-                    if (rfl((uint32_t)__hip_atomic_load(a.activity + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                        leave = 1;
-                        break;
-                    }
+        // stagger the waves' polls by ~1/4 of a PCIe round trip
+        if (wave == 1) __builtin_amdgcn_s_sleep(12);
+        if (wave == 2) __builtin_amdgcn_s_sleep(24);
+        if (wave == 3) __builtin_amdgcn_s_sleep(36);
+        uint32_t polls = 0;
+        for (;;) {
+            uint64_t gv = 0;
+            if (lane < 8) gv = __hip_atomic_load(&ms->req.g[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const bool ok = lane >= 8 || (uint32_t)(gv >> 32) == want;
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0) {  // all eight granules carry the number
+                if (lane < 8) sreq[lane] = (uint32_t)gv;
+                if (lane == 0) sfound = want;  // (several waves may find it: same bytes)
+                break;
+            }
+            const uint32_t f = rfl(sfound);
+            if (f == want || f == ~0u) break;  // another wave found it, or the launch closes
+            if (wave == 0 && (++polls & 63u) == 0) {
+                // the launch closes as a whole: once one workgroup found every
+                // slot idle for idle_ticks it raises `closing`, and the others
+                // follow within a few polls (a caller whose slot was left
+                // waits for the whole launch to end, then relaunches it)
+                bool leave = rfl((uint32_t)__hip_atomic_load(a.activity + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
+                if (!leave) {
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     uint64_t act = __hip_atomic_load(a.activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     act = rfl((uint32_t)act) | ((uint64_t)rfl((uint32_t)(act >> 32)) << 32);
                     const uint64_t ref = act > t_last ? act : t_last;
-                    if (now > ref && now - ref > a.idle_ticks) {
-                        if (t == 0) __hip_atomic_store(a.activity + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        leave = 1;
-                        break;
-                    }
+                    leave = now > ref && now - ref > a.idle_ticks;
+                    if (leave && lane == 0)
+                        __hip_atomic_store(a.activity + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                __builtin_amdgcn_s_sleep(1);
+                if (leave) {
+                    if (lane == 0) sfound = ~0u;
+                    break;
+                }
             }
-            if (t == 0) sexit = leave;
+            __builtin_amdgcn_s_sleep(4);
         }
         __syncthreads();
-        const uint32_t leave = rfl(sexit);
+        const uint32_t found = rfl(sfound);
         const uint32_t op = rfl(sreq[kWfOp]);
-        __syncthreads();  // sreq / sexit are rewritten by the next poll
-        if (leave || op > kWopDecode) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        if (found != want || op > kWopDecode) {
             // idle (or a stop request): tell the host this slot's workgroup is gone
             if (t == 0) {
-                if (!leave) __hip_atomic_store(a.activity + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!leave) __hip_atomic_store(&ms->resp.done, (uint64_t)want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (found == want) {  // a stop request: answer it, close the launch
+                    __hip_atomic_store(a.activity + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ms->resp.done, (uint64_t)want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 __hip_atomic_store(&ms->resp.exited, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             return;
         }
-        const uint32_t S = rfl(sreq[kWfShardLen]), mask = rfl(sreq[kWfMask]), pitch = rfl(sreq[kWfPitch]);
+        const uint32_t S = rfl(sreq[kWfShardLen]), mask = rfl(sreq[kWfMask]) & a.nmask, pitch = rfl(sreq[kWfPitch]);
         const uint64_t inb = (uint64_t)rfl(sreq[kWfInLo]) | ((uint64_t)rfl(sreq[kWfInHi]) << 32);
         const uint64_t outb = (uint64_t)rfl(sreq[kWfOutLo]) | ((uint64_t)rfl(sreq[kWfOutHi]) << 32);
+        __syncthreads();  // sreq is rewritten by the next poll
+
+        // input rows, ascending: Encode the data rows, Verify every row,
+        // Reconstruct(Data) the first k present rows, the fused decode every
+        // present row (survivors, then the extras its check rows compare)
+        uint32_t rows = a.nmask;
+        if (op <= kWopEncodeVerify) {
+            rows = (1u << a.k) - 1u;
+        } else if (op == kWopDecode) {
+            rows = mask;
+        } else if (op != kWopVerify) {
+            uint32_t m = mask;
+            rows = 0;
+            for (uint32_t i = 0; i < a.k && m; ++i) {
+                const uint32_t b = m & (0u - m);
+                rows |= b;
+                m ^= b;
+            }
+        }
+        const uint32_t kact = (uint32_t)__builtin_popcount(rows);
+        const uint32_t nvec = (S + 15) / 16, tail = S - (nvec - 1) * 16;
+        const uint32_t wlast = pitch - (nvec - 1) * 16, part = wlast < 16 ? wlast : 0u;
+        const uint32_t span = (a.n - 1) * pitch + nvec * 16;
+        const __amdgpu_buffer_rsrc_t rsi = __builtin_amdgcn_make_buffer_rsrc((void *)inb, (short)0, (int)span, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc((void *)outb, (short)0, (int)span, 0x00020000);
+        // lane-parallel geometry: vc vectors per pass, np passes
+        const uint32_t vc = kact ? (256u / kact < kLaneVecs ? 256u / kact : kLaneVecs) : 1u;
+        const uint32_t np = (nvec + vc - 1) / vc;
+        const bool lanepar = np <= kLaneU;
+        const uint32_t my_c = t / vc, my_v = t - my_c * vc;  // lane-parallel role: (input, vector)
+        const bool in_lane = my_c < kact;
+        const uint32_t my_row = nth_bit(rows, my_c);
+
+        u32x4 x[kWorkerMaxN];  // lane = vector: every input
+        u32x4 xl[kLaneU];      // lane-parallel: this lane's input, one vector per pass
+        auto load_chunk = [&](uint32_t c0) {  // lane = vector c0 + t, every input
+            const uint32_t v = c0 + t;
+            const uint32_t voff = v < nvec ? v * 16u : 0xfffffff0u;  // past every range: reads 0
+            uint32_t m = rows;
+#pragma unroll
+            for (int c = 0; c < (int)kWorkerMaxN; ++c) {
+                const uint32_t row = m ? (uint32_t)__builtin_ctz(m) : 0u;
+                m &= m - 1u;
+                x[c] = u32x4{0u, 0u, 0u, 0u};
+                if ((uint32_t)c < kact) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, voff, row * pitch, kSysAux);
+            }
+        };
+        if (lanepar) {
+#pragma unroll
+            for (uint32_t u = 0; u < kLaneU; ++u) {
+                const uint32_t v = u * vc + my_v;
+                xl[u] = u32x4{0u, 0u, 0u, 0u};
+                if (u < np && in_lane && v < nvec)
+                    xl[u] = __builtin_amdgcn_raw_buffer_load_b128(rsi, v * 16u, my_row * pitch, kSysAux);
+            }
+        } else {
+            load_chunk(0);
+        }
+        asm volatile("" ::: "memory");  // the loads go out before the lookup below waits
 
         // the operation's records (uniform, scalar loads from device memory)
         constant_ptr<PatRec> rec = nullptr;
@@ -108,94 +203,166 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
             nsub = a.ver_nsub;
         } else {
             const uint32_t m = op - kWopReconstruct;
-            const int32_t slot = ((constant_ptr<int32_t>)a.pat[m])[mask & a.nmask];
+            const int32_t slot = ((constant_ptr<int32_t>)a.pat[m])[mask];
             if (slot >= 0) {  // else nothing to do (the host rejected too-few / singular patterns)
                 nsub = a.nsub[m];
                 rec = (constant_ptr<PatRec>)a.recs[m] + (uint32_t)slot * nsub;
             }
         }
+        uint64_t t1 = 0, t2 = 0, t3 = 0, t4 = 0;  // trace: loaded, computed, stored, read back
         bool mismatch = false;
-        if (nsub) {
-            const uint32_t nvec = (S + 15) / 16, tail = S - (nvec - 1) * 16;
-            const uint32_t wlast = pitch - (nvec - 1) * 16, part = wlast < 16 ? wlast : 0u;
-            const uint32_t span = (a.n - 1) * pitch + nvec * 16;
-            const __amdgpu_buffer_rsrc_t rsi = __builtin_amdgcn_make_buffer_rsrc((void *)inb, (short)0, (int)span, 0x00020000);
-            const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc((void *)outb, (short)0, (int)span, 0x00020000);
-            const constant_ptr<uint32_t> r0 = (constant_ptr<uint32_t>)rec;
-            const uint32_t kact = r0[0] & 0xffu;
-            const uint32_t irow[4] = {r0[20], r0[21], r0[22], r0[23]};
-            for (uint32_t c0 = 0; c0 < nvec; c0 += 256) {
-                const uint32_t v = c0 + t;
-                const bool live = v < nvec;
-                const uint32_t voff = live ? v * 16u : 0xfffffff0u;  // past every range: reads 0, stores dropped
-                u32x4 x[kWorkerMaxN];
+        if (nsub && lanepar) {
 #pragma unroll
-                for (int c = 0; c < (int)kWorkerMaxN; ++c) {
-                    x[c] = u32x4{0u, 0u, 0u, 0u};
-                    if ((uint32_t)c < kact)
-                        x[c] = __builtin_amdgcn_raw_buffer_load_b128(rsi, voff, ((irow[c >> 2] >> (8 * (c & 3))) & 0xffu) * pitch,
-                                                                     kSysAux);
+            for (uint32_t u = 0; u < kLaneU; ++u) {  // compile-time index into xl[] (a runtime one puts it in scratch)
+              if (u < np) {
+                if (a.trace && u == 0) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    t1 = __builtin_amdgcn_s_memrealtime();
                 }
+                GfIdx g[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) g[d] = gf_idx(xl[u][d]);
                 for (uint32_t s = 0; s < nsub; ++s) {
                     const constant_ptr<uint32_t> rw = (constant_ptr<uint32_t>)(rec + s);
                     const uint32_t h0 = rw[0], orow = rw[2];
                     const uint32_t nr = (h0 >> 8) & 0xffu, nw = (h0 >> 16) & 0xffu;
-                    uint32_t acc[4][4];
+                    // this lane's input times every row of the sub-pass -> LDS
+                    if (in_lane && my_v < vc) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
+                        for (int r = 0; r < RM; ++r) {
+                            const uint32_t q = my_c >> 2;
+                            const uint32_t w0 = rw[4 + r * 4], w1 = rw[5 + r * 4], w2 = rw[6 + r * 4], w3 = rw[7 + r * 4];
+                            const uint32_t cw = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+                            const uint32_t cf = (cw >> (8 * (my_c & 3))) & 0xffu;
+                            const u32x4 tw = lt[cf][0];
+                            const uint32_t t4w = lt[cf][1][0];
+                            u32x4 pr;
 #pragma unroll
-                        for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+                            for (int d = 0; d < 4; ++d) pr[d] = gf_mac_w(0u, tw, t4w, g[d]);
+                            red[r][my_c][my_v] = pr;
+                        }
+                    }
+                    __syncthreads();
+                    if (a.trace && u == 0 && s == 0) t2 = __builtin_amdgcn_s_memrealtime();
+                    // lane = (row, vector): XOR over the inputs, then store or check
+                    const uint32_t r = t / vc, vv = t - r * vc, v = u * vc + vv;
+                    u32x4 acc = {0u, 0u, 0u, 0u};
+                    if (r < nr && vv < vc && v < nvec) {
+                        for (uint32_t c = 0; c < kact; ++c) acc ^= red[r][c][vv];
+                        const uint32_t valid = v == nvec - 1 ? tail : 16u;
+                        if (r < nw) {
+                            const uint32_t row = (orow >> (8 * r)) & 0xffu;
+                            store_row<kSysAux>(acc, rso, v * 16u, row * pitch, v == nvec - 1 ? part : 0u);
+                            if (op == kWopEncodeVerify) {
+                                // Verify on the parity rows as stored: the store
+                                // completes, then the row is read back over PCIe
+                                // (a read does not pass the posted writes before it)
+                                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                if (a.trace && u == 0 && s == 0 && t == 0) t3 = __builtin_amdgcn_s_memrealtime();
+                                const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rso, v * 16u, row * pitch, kSysAux);
 #pragma unroll
-                    for (int c = 0; c < (int)kWorkerMaxN; ++c) {
-                        if ((uint32_t)c < kact) {
-                            GfIdx g[4];
-#pragma unroll
-                            for (int d = 0; d < 4; ++d) g[d] = gf_idx(x[c][d]);
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const uint32_t cf = (rw[4 + r * 4 + (c >> 2)] >> (8 * (c & 3))) & 0xffu;
-                                const u32x4 tw = lt[cf][0];
-                                const uint32_t t4 = lt[cf][1][0];
-#pragma unroll
-                                for (int d = 0; d < 4; ++d) acc[r][d] = gf_mac_w(acc[r][d], tw, t4, g[d]);
+                                for (int d = 0; d < 4; ++d) mismatch |= ((b[d] ^ acc[d]) & tail_mask(d, valid)) != 0;
+                                if (a.trace && u == 0 && s == 0 && t == 0) t4 = __builtin_amdgcn_s_memrealtime();
                             }
+                        } else {
+#pragma unroll
+                            for (int d = 0; d < 4; ++d) mismatch |= (acc[d] & tail_mask(d, valid)) != 0;
                         }
                     }
-                    const uint32_t valid = v == nvec - 1 ? tail : 16u;
+                    __syncthreads();  // red is rewritten by the next sub-pass / pass
+                }
+              }
+            }
+        }
+        for (uint32_t c0 = 0; nsub && !lanepar;) {  // larger objects: lane = vector
+            const uint32_t v = c0 + t;
+            const bool live = v < nvec;
+            const uint32_t voff = live ? v * 16u : 0xfffffff0u;  // stores there are dropped
+            const uint32_t valid = v == nvec - 1 ? tail : 16u;
+            if (a.trace && c0 == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                t1 = __builtin_amdgcn_s_memrealtime();
+            }
+            for (uint32_t s = 0; s < nsub; ++s) {
+                const constant_ptr<uint32_t> rw = (constant_ptr<uint32_t>)(rec + s);
+                const uint32_t h0 = rw[0], orow = rw[2];
+                const uint32_t nr = (h0 >> 8) & 0xffu, nw = (h0 >> 16) & 0xffu;
+                uint32_t acc[RM][4];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        if ((uint32_t)r >= nr) continue;
-                        if ((uint32_t)r < nw) {
-                            const uint32_t row = (orow >> (8 * r)) & 0xffu;
-                            const u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-                            store_row<kSysAux>(o, rso, voff, row * pitch, v == nvec - 1 ? part : 0u);
-                        } else if (live) {
+                for (int r = 0; r < RM; ++r)
 #pragma unroll
-                            for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+                    for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+#pragma unroll
+                for (int c = 0; c < (int)kWorkerMaxN; ++c) {
+                    if ((uint32_t)c < kact) {
+                        GfIdx g[4];
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) g[d] = gf_idx(x[c][d]);
+#pragma unroll
+                        for (int r = 0; r < RM; ++r) {
+                            const uint32_t cf = (rw[4 + r * 4 + (c >> 2)] >> (8 * (c & 3))) & 0xffu;
+                            const u32x4 tw = lt[cf][0];
+                            const uint32_t t4w = lt[cf][1][0];
+#pragma unroll
+                            for (int d = 0; d < 4; ++d) acc[r][d] = gf_mac_w(acc[r][d], tw, t4w, g[d]);
                         }
                     }
-                    if (op == kWopEncodeVerify && nw > 0) {
-                        // Verify on the parity rows as stored: this wave's stores
-                        // complete, then the rows read back over PCIe (a read does
-                        // not pass the posted writes before it) and compared
+                    // input at a time (the table reads are not all hoisted)
+#pragma unroll
+                    for (int r = 0; r < RM; ++r)
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (a.trace && c0 == 0 && s == 0) t2 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+                for (int r = 0; r < RM; ++r) {
+                    if ((uint32_t)r >= nr) continue;
+                    if ((uint32_t)r < nw) {
+                        const uint32_t row = (orow >> (8 * r)) & 0xffu;
+                        const u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+                        store_row<kSysAux>(o, rso, voff, row * pitch, v == nvec - 1 ? part : 0u);
+                    } else if (live) {
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+                    }
+                }
+                if (op == kWopEncodeVerify && nw > 0) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (a.trace && c0 == 0 && s == 0) t3 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+                    for (int r = 0; r < RM; ++r) {
+                        if ((uint32_t)r >= nw) continue;
+                        const uint32_t row = (orow >> (8 * r)) & 0xffu;
+                        const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rso, voff, row * pitch, kSysAux);
+                        if (live)
+#pragma unroll
+                            for (int d = 0; d < 4; ++d) mismatch |= ((b[d] ^ acc[r][d]) & tail_mask(d, valid)) != 0;
+                    }
+                    if (a.trace && c0 == 0 && s == 0) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            if ((uint32_t)r >= nw) continue;
-                            const uint32_t row = (orow >> (8 * r)) & 0xffu;
-                            const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rso, voff, row * pitch, kSysAux);
-                            if (live)
-#pragma unroll
-                                for (int d = 0; d < 4; ++d) mismatch |= ((b[d] ^ acc[r][d]) & tail_mask(d, valid)) != 0;
-                        }
+                        t4 = __builtin_amdgcn_s_memrealtime();
                     }
                 }
             }
+            c0 += 256;
+            if (c0 >= nvec) break;
+            load_chunk(c0);
         }
         // every wave's stores complete before the response is published
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (a.trace && !t3) t3 = __builtin_amdgcn_s_memrealtime();
         const int bad = __syncthreads_or(mismatch);
         if (t == 0) {
+            if (a.trace) {  // stamps (s_memrealtime ticks of 10 ns) after the request was seen
+                const uint64_t t5 = __builtin_amdgcn_s_memrealtime();
+                ms->resp.pad[0] = (uint32_t)(t1 ? t1 - t0 : 0);
+                ms->resp.pad[1] = (uint32_t)(t2 ? t2 - t0 : 0);
+                ms->resp.pad[2] = (uint32_t)(t3 ? t3 - t0 : 0);
+                ms->resp.pad[3] = (uint32_t)(t4 ? t4 - t0 : 0);
+                ms->resp.pad[4] = (uint32_t)(t5 - t0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __hip_atomic_store(&ms->resp.done, (uint64_t)want | ((uint64_t)(bad ? 1u : 0u) << 32), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(a.activity, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -222,12 +389,18 @@ struct Worker {
     hipStream_t stream = nullptr;                       // its own hardware queue (CU-mask stream)
     uint64_t *d_state = nullptr;                        // [0] activity (realtime), [1] closing
     void *d_enc = nullptr, *d_ver = nullptr;            // Encode / Verify records
-    uint32_t enc_nsub = 0, ver_nsub = 0;
+    uint32_t *d_enc_tab = nullptr, *d_ver_tab = nullptr;  // their v_perm tables [nsub][K][R][5]
+    uint32_t enc_nsub = 0, ver_nsub = 0, enc_r = 0, ver_r = 0;
+    int rm = 4;                                         // kernel instantiation: min(4, parity)
     AtlasView views[3];
     uint64_t idle_ticks = 0;
     std::mutex mu;                                      // launches
     std::atomic<uint32_t> gen{1};                       // the launch the mailboxes belong to
     std::atomic<uint64_t> served{0}, declined{0}, launches{0};  // rsgpu_worker_stats
+    int k = 0;
+    bool trace = false;                                 // RSGPU_WORKER_TRACE: device stamps per request
+    // trace sums per op: [op][0] requests, [1..5] device stamps (10 ns), [6] host post->response (ns)
+    std::atomic<uint64_t> tr[6][7] = {};
     ~Worker() {
         if (stream) (void)hipStreamDestroy(stream);
         if (h_slots) (void)hipHostFree(h_slots);
@@ -236,6 +409,8 @@ struct Worker {
         if (d_state) (void)hipFree(d_state);
         if (d_enc) (void)hipFree(d_enc);
         if (d_ver) (void)hipFree(d_ver);
+        if (d_enc_tab) (void)hipFree(d_enc_tab);
+        if (d_ver_tab) (void)hipFree(d_ver_tab);
     }
 };
 
@@ -270,6 +445,16 @@ std::vector<PatRec> plan_records(const Plan &p) {
     return recs;
 }
 
+// v_perm tables of those records, [nsub][K][R][kTabWords], R = min(4, plan rows)
+std::vector<uint32_t> record_tables(const std::vector<PatRec> &recs, int K, int R) {
+    std::vector<uint32_t> t(recs.size() * K * R * kTabWords, 0);
+    for (size_t s = 0; s < recs.size(); ++s)
+        for (int c = 0; c < K; ++c)
+            for (int r = 0; r < R; ++r)
+                coef_tables(recs[s].coef[r][c], &t[(((s * K) + c) * R + r) * kTabWords]);
+    return t;
+}
+
 hipError_t upload(const std::vector<PatRec> &r, void *&d) {
     hipError_t e = hipMalloc(&d, r.size() * sizeof(PatRec));
     if (e == hipSuccess) e = hipMemcpy(d, r.data(), r.size() * sizeof(PatRec), hipMemcpyHostToDevice);
@@ -283,10 +468,17 @@ hipError_t launch(Worker &w, uint32_t g) {
     for (int m = 0; m < 3; ++m) {
         a.pat[m] = w.views[m].pat;
         a.recs[m] = w.views[m].recs;
+        a.tabs[m] = w.views[m].tabs;
         a.nsub[m] = (uint32_t)w.views[m].nsub;
+        a.tk[m] = (uint32_t)w.views[m].kmax;
+        a.tr[m] = (uint32_t)w.views[m].R;
     }
     a.enc_rec = w.d_enc;
     a.ver_rec = w.d_ver;
+    a.enc_tab = w.d_enc_tab;
+    a.ver_tab = w.d_ver_tab;
+    a.enc_r = w.enc_r;
+    a.ver_r = w.ver_r;
     a.enc_nsub = w.enc_nsub;
     a.ver_nsub = w.ver_nsub;
     a.ctab = w.views[0].ctab;
@@ -295,9 +487,16 @@ hipError_t launch(Worker &w, uint32_t g) {
     a.gen = g;
     a.n = (uint32_t)w.views[0].n;
     a.nmask = (uint32_t)((1u << w.views[0].n) - 1);
+    a.k = (uint32_t)w.k;
+    a.trace = w.trace ? 1u : 0u;
     hipError_t e = hipMemsetAsync(w.d_state, 0, 16, w.stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gf_worker, dim3(w.nslots), dim3(256), 0, w.stream, a);
+    switch (w.rm) {
+        case 1: hipLaunchKernelGGL(gf_worker<1>, dim3(w.nslots), dim3(256), 0, w.stream, a); break;
+        case 2: hipLaunchKernelGGL(gf_worker<2>, dim3(w.nslots), dim3(256), 0, w.stream, a); break;
+        case 3: hipLaunchKernelGGL(gf_worker<3>, dim3(w.nslots), dim3(256), 0, w.stream, a); break;
+        default: hipLaunchKernelGGL(gf_worker<4>, dim3(w.nslots), dim3(256), 0, w.stream, a); break;
+    }
     return hipGetLastError();
 }
 
@@ -305,6 +504,8 @@ int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard
     std::unique_ptr<Worker> w(new Worker());
     w->nslots = nslots;
     w->max_shard = max_shard;
+    w->k = ctx->k;
+    w->trace = std::getenv("RSGPU_WORKER_TRACE") != nullptr;
     w->idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
     for (int m = 0; m < 3; ++m) {
         int e = ctx->atlas_view((AtlasMode)m, w->views[m]);
@@ -313,8 +514,17 @@ int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard
     std::vector<PatRec> er = plan_records(*ctx->plan_encode()), vr = plan_records(*ctx->plan_verify());
     w->enc_nsub = (uint32_t)er.size();
     w->ver_nsub = (uint32_t)vr.size();
+    w->rm = std::min(4, ctx->p);
+    w->enc_r = w->ver_r = (uint32_t)w->rm;
+    for (int m = 0; m < 3; ++m)
+        if (w->views[m].R > w->rm) return RSGPU_ERR_INVALID_ARG;  // (atlas rows per sub-pass <= min(4, p))
     HIP_TRY(upload(er, w->d_enc));
     HIP_TRY(upload(vr, w->d_ver));
+    const std::vector<uint32_t> et = record_tables(er, ctx->k, w->rm), vt = record_tables(vr, ctx->n, w->rm);
+    HIP_TRY(hipMalloc(&w->d_enc_tab, et.size() * 4));
+    HIP_TRY(hipMemcpy(w->d_enc_tab, et.data(), et.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&w->d_ver_tab, vt.size() * 4));
+    HIP_TRY(hipMemcpy(w->d_ver_tab, vt.data(), vt.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&w->d_state, 16));
     // a CU-masked stream is its own hardware queue: no other stream's work
     // queues behind the resident kernel
@@ -358,11 +568,19 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
     for (int g = 0; g < 8; ++g)
         __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)n << 32), __ATOMIC_RELEASE);
     uint32_t cur = w.gen.load(std::memory_order_acquire);
+    const auto t_post = std::chrono::steady_clock::now();
     unsigned spins = 0;
     for (;;) {
         const uint64_t d = __atomic_load_n(&s.resp.done, __ATOMIC_ACQUIRE);
         if ((uint32_t)d == n) {
             status = (uint32_t)(d >> 32);
+            if (w.trace && rq[kWfOp] < 6) {
+                auto &tr = w.tr[rq[kWfOp]];
+                tr[0].fetch_add(1);
+                for (int j = 0; j < 5; ++j) tr[1 + j].fetch_add(s.resp.pad[j]);
+                tr[6].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                    std::chrono::steady_clock::now() - t_post).count());
+            }
             return RSGPU_OK;
         }
         if (__atomic_load_n(&s.resp.exited, __ATOMIC_ACQUIRE) == cur) {
@@ -458,6 +676,20 @@ int worker_stop(rsgpu_ctx *ctx) {
     const hipError_t he = hipStreamSynchronize(w->stream);
     if (he != hipSuccess) e = hip_fail(he, "worker stop");
     w->free_mask.store(all);
+    if (w->trace) {
+        static const char *names[6] = {"encode", "encode+verify", "verify", "reconstruct", "reconstruct-data", "decode"};
+        for (int op = 0; op < 6; ++op) {
+            const uint64_t nreq = w->tr[op][0].load();
+            if (!nreq) continue;
+            auto avg = [&](int j, double unit) { return w->tr[op][j].load() * unit / nreq; };
+            std::fprintf(stderr,
+                         "rsgpu worker trace %-16s %7llu requests; avg us after the request was seen: inputs "
+                         "loaded %.2f, computed %.2f, stores done %.2f, read back %.2f, response %.2f; host post -> "
+                         "response %.2f\n",
+                         names[op], (unsigned long long)nreq, avg(1, 0.01), avg(2, 0.01), avg(3, 0.01), avg(4, 0.01),
+                         avg(5, 0.01), avg(6, 0.001));
+        }
+    }
     return e;
 }
 

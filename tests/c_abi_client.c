@@ -162,11 +162,13 @@ static int gpu_checks(void) {
  *   succeeds, the second Verify is false -> decode's error path.  The fused
  *   forms (rsgpu_encode_verify_image, rsgpu_decode_image) give the same
  *   booleans and bytes. */
-static int ecredis_replay(void) {
+static int ecredis_replay(size_t N, int worker) {
     const int k = 10, p = 2, n = 12;
-    const size_t N = 1 << 20, S = (N + k - 1) / k;
+    const size_t S = (N + k - 1) / k;
     rsgpu_ctx *ctx;
     CHECK(rsgpu_create(k, p, RSGPU_ALL_DEVICES, 0, &ctx) == RSGPU_OK);
+    /* the resident worker serves the same calls (rsgpu_worker_start) */
+    if (worker) CHECK(rsgpu_worker_start(ctx, 4, 0, 0) == RSGPU_OK);
     uint8_t *obj = malloc(N);
     for (size_t j = 0; j < N; j++) obj[j] = rnd8();
     /* ---- Client.encode (ecRedis.go:382-402) */
@@ -202,7 +204,7 @@ static int ecredis_replay(void) {
             got[10] = malloc(S);
             memcpy(got[10], split + 10 * S, S);
             lens[10] = S;
-            got[11][777] ^= 0x20;
+            got[11][S / 2] ^= 0x20;
         }
         /* stats.AllGood, _ = Verify(data): nil shards -> (false, ErrShardSize) */
         ok = 7;
@@ -256,13 +258,21 @@ static int ecredis_replay(void) {
     free(split);
     free(split2);
     free(obj);
+    if (worker) {
+        uint64_t served = 0, declined = 0, launches = 0;
+        CHECK(rsgpu_worker_stats(ctx, &served, &declined, &launches) == RSGPU_OK);
+        CHECK(served >= 9 && launches >= 1);  /* 3 encode-side + 3 per Get trial */
+        printf("worker: %llu calls served, %llu launches\n", (unsigned long long)served, (unsigned long long)launches);
+    }
     rsgpu_destroy(ctx);
-    printf("ecredis replay ok (Client.encode/decode call order, contiguous and staged routes)\n");
+    printf("ecredis replay ok (%zu-B object%s; Client.encode/decode call order, contiguous and staged routes)\n", N,
+           worker ? ", resident worker" : "");
     return 0;
 }
 
 int main(int argc, char **argv) {
     if (host_checks()) return 1;
-    if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_checks() || ecredis_replay();
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0)
+        return gpu_checks() || ecredis_replay(1 << 20, 0) || ecredis_replay(1024, 1);
     return 0;
 }
