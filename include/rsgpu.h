@@ -166,7 +166,8 @@ int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
  *   idle_us    the kernel leaves after this long without any request (0: 50 ms)
  *              and the next call relaunches it; while it runs, a
  *              hipDeviceSynchronize in the process waits for it to leave
- *   max_shard  the largest shard_len served (0: 16 KiB)
+ *   max_shard  the largest shard_len served (0: 4 KiB; the worker is ahead of the
+ *              stream path up to ~40 KB objects and level with it at 64 KiB)
  * Calling it again restarts the worker with the new settings.  Multi-device
  * contexts: one worker per entry.  Requires data+parity <= 16
  * (RSGPU_ERR_NOT_IMPLEMENTED otherwise). */

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 namespace rsgpu {
 
@@ -104,6 +105,18 @@ struct Pass {
     uint32_t tab[K * R * kTabWords];  // input-major [K][R][kTabWords]: scalar loads per input
 };
 
+// A pass whose GF inputs go in triples (gf_apply_body<..., TRI = true>): the
+// 24 index bits of inputs a, b, c are eight 3-bit groups, bits [2:0] and
+// [5:3] of each input plus {a[7:6], b[7]} and {b[6], c[7:6]}; each group is
+// one v_perm lookup into an 8-entry table of its row (the two cross groups'
+// tables mix two coefficients, as the generic kernel's, gf_kernels.hip).
+// Per row and dword 8 v_perm + 4 xor3 for three inputs instead of 9 + 6.
+template <int K, int R>
+struct Pass3 : Pass<K, R> {
+    uint32_t ntrip;  // inputs [0, 3 * ntrip) go in triples, the rest one at a time
+    uint32_t tab3[(K / 3 > 0 ? K / 3 : 1) * R * 16];  // [t][r]: words 0-7 entries 0-3, 8-15 entries 4-7
+};
+
 // Workgroup -> (item, chunk) order of a 1D launch over `total` = nitem x
 // nchunk workgroups.  The hardware deals workgroup ids round-robin to the 8
 // XCDs (id % 8), and each XCD translates through its own TLB.
@@ -124,7 +137,7 @@ __device__ __forceinline__ bool wg_item(const Order &o, uint32_t &item, uint32_t
     return true;
 }
 
-template <int K, int R>
+template <int K, int R, typename PT = Pass<K, R>>
 struct ApplyArgs {  // one pass for every object of the launch (kernarg)
     const uint8_t *base;
     // per-object host API (one object, rsgpu.cpp run_host): the rows may be
@@ -142,7 +155,7 @@ struct ApplyArgs {  // one pass for every object of the launch (kernarg)
     uint32_t nobj;   // objects in the launch (bounds the last group when opw > 1)
     uint32_t gspan;  // opw > 1: bytes a group's objects cover from the first one's base
     Order ord;       // item = object, or group of opw objects
-    Pass<K, R> p;
+    PT p;
 };
 
 template <int K, int R>
@@ -190,7 +203,7 @@ struct Redirect {
 // Variable-size batches (VAR = true, gf_apply_var): the pass's in_off /
 // out_off hold row INDICES, scaled by the object's own pitch `vp`; `span` is
 // the object's own span and `vpacked` its store_row part.
-template <int K, int R, int U, int BS, int LAUX, int SAUX, typename P, bool VAR = false>
+template <int K, int R, int U, int BS, int LAUX, int SAUX, typename P, bool VAR = false, bool TRI = false>
 __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P &a,
                                               uint32_t nvec, uint32_t tail, uint32_t *bad,
                                               uint32_t v0, const Redirect &rd = Redirect(),
@@ -233,8 +246,47 @@ __device__ __forceinline__ void gf_apply_body(const uint8_t *ob, uint32_t obj, P
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+        uint32_t ntr = 0;
+        if constexpr (TRI) {  // GF inputs in triples (Pass3)
+            ntr = a.ntrip;
+#pragma unroll
+            for (int tt = 0; tt < K / 3; ++tt) {
+                if ((uint32_t)tt < ntr) {
+                    uint32_t sel[4][8];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        const uint32_t xa = x[u][3 * tt][d], xb = x[u][3 * tt + 1][d], xc = x[u][3 * tt + 2][d];
+                        sel[d][0] = xa & 0x07070707u;
+                        sel[d][1] = (xa >> 3) & 0x07070707u;
+                        sel[d][2] = xb & 0x07070707u;
+                        sel[d][3] = (xb >> 3) & 0x07070707u;
+                        sel[d][4] = xc & 0x07070707u;
+                        sel[d][5] = (xc >> 3) & 0x07070707u;
+                        sel[d][6] = ((xa >> 5) & 0x06060606u) | ((xb >> 7) & 0x01010101u);
+                        sel[d][7] = ((xb >> 6) & 0x01010101u) | ((xc >> 5) & 0x06060606u);
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const auto *T = &a.tab3[(tt * R + r) * 16];
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) {
+                            uint32_t q = xor3(acc[r][d], lut8(T[0], T[8], sel[d][0]), lut8(T[1], T[9], sel[d][1]));
+                            q = xor3(q, lut8(T[2], T[10], sel[d][2]), lut8(T[3], T[11], sel[d][3]));
+                            q = xor3(q, lut8(T[4], T[12], sel[d][4]), lut8(T[5], T[13], sel[d][5]));
+                            acc[r][d] = xor3(q, lut8(T[6], T[14], sel[d][6]), lut8(T[7], T[15], sel[d][7]));
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(acc[r][d]));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
 #pragma unroll
         for (int c = 0; c < K; ++c) {
+            if (TRI && (uint32_t)c < 3 * ntr) continue;  // coded in its triple
             if (c >= K - R && c >= K - (int)a.ki) {
                 // identity input: row R-K+c (compile-time index) ^= input
 #pragma unroll
@@ -308,16 +360,17 @@ constexpr int kFormAny = 0;       // runtime: small objects if a.opw > 1, else c
 constexpr int kFormChunks = 1;    // one object per workgroup chunk, no redirection
 constexpr int kFormSmall = 2;     // a.opw > 1 objects per workgroup
 constexpr int kFormRedirect = 3;  // one object, zero-copy redirection (per-object host API)
-template <int K, int R, int U, int BS, int LAUX, int SAUX, int FORM = kFormAny>
-__global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
+template <int K, int R, int U, int BS, int LAUX, int SAUX, int FORM = kFormAny, bool TRI = false>
+__global__ __launch_bounds__(BS) void gf_apply_kernel(
+    const ApplyArgs<K, R, std::conditional_t<TRI, Pass3<K, R>, Pass<K, R>>> a) {
     uint32_t obj, chunk;
     if (!wg_item(a.ord, obj, chunk)) return;
     if (FORM == kFormSmall || (FORM == kFormAny && a.opw > 1)) {  // small objects: lane -> (object j of the group, vector v)
         const uint32_t j = threadIdx.x / a.nvec, o0 = obj * a.opw;
         if (j >= a.opw || o0 + j >= a.nobj) return;
-        gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)o0 * a.obj_stride, o0 + j, a.p, a.nvec,
-                                               a.tail, a.bad, threadIdx.x - j * a.nvec, Redirect(),
-                                               j * (uint32_t)a.obj_stride, a.gspan);
+        gf_apply_body<K, R, U, BS, LAUX, SAUX, const decltype(a.p), false, TRI>(
+            a.base + (uint64_t)o0 * a.obj_stride, o0 + j, a.p, a.nvec, a.tail, a.bad, threadIdx.x - j * a.nvec,
+            Redirect(), j * (uint32_t)a.obj_stride, a.gspan);
         return;
     }
     Redirect rd;
@@ -328,8 +381,9 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(const ApplyArgs<K, R> a) {
         rd.out = a.out_base;
         rd.dual = a.out_dual != 0;
     }
-    gf_apply_body<K, R, U, BS, LAUX, SAUX>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p, a.nvec,
-                                           a.tail, a.bad, chunk * (BS * U) + threadIdx.x, rd);
+    gf_apply_body<K, R, U, BS, LAUX, SAUX, const decltype(a.p), false, TRI>(a.base + (uint64_t)obj * a.obj_stride, obj, a.p,
+                                                                       a.nvec, a.tail, a.bad,
+                                                                       chunk * (BS * U) + threadIdx.x, rd);
 }
 
 // constant address space: uniform invariant data the compiler may (and does)

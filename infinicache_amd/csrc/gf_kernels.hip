@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -341,9 +342,80 @@ void fill_pass(const Plan &p, const Sub &s, size_t pitch, size_t space, uint32_t
     a.span = (uint32_t)((size_t)maxrow * pitch + (size_t)nvec * 16);
 }
 
+// Input-triple tables of a sub-pass (Pass3): the GF inputs [0, K - ki) in
+// triples, entries of the 8 tables per (triple, row) as gf_apply_body reads them
+template <int K, int R>
+void fill_triples(const Plan &p, const Sub &s, Pass3<K, R> &a) {
+    const GF &g = gf();
+    a.ntrip = (uint32_t)((K - (int)a.ki) / 3);
+    std::memset(a.tab3, 0, sizeof(a.tab3));
+    for (uint32_t t = 0; t < a.ntrip; ++t)
+        for (int r = 0; r < R; ++r) {
+            const size_t row = (size_t)(s.r0 + r) * K;
+            const uint8_t ca = p.coef[row + 3 * t], cb = p.coef[row + 3 * t + 1], cc = p.coef[row + 3 * t + 2];
+            uint32_t *w = &a.tab3[((size_t)t * R + r) * 16];
+            for (int j = 0; j < 8; ++j) {
+                const uint8_t ent[8] = {
+                    g.mul(ca, (uint8_t)j), g.mul(ca, (uint8_t)(j << 3)), g.mul(cb, (uint8_t)j), g.mul(cb, (uint8_t)(j << 3)),
+                    g.mul(cc, (uint8_t)j), g.mul(cc, (uint8_t)(j << 3)),
+                    (uint8_t)(g.mul(ca, (uint8_t)((j >> 1) << 6)) ^ g.mul(cb, (uint8_t)((j & 1) << 7))),
+                    (uint8_t)(g.mul(cb, (uint8_t)((j & 1) << 6)) ^ g.mul(cc, (uint8_t)((j >> 1) << 6)))};
+                for (int q = 0; q < 8; ++q) w[q + (j >> 2) * 8] |= (uint32_t)ent[q] << (8 * (j & 3));
+            }
+        }
+}
+
+// Check-only passes of >= 3 rows are VALU-bound (Verify RS(10+4): 14 inputs
+// x 4 check rows): their GF inputs go in triples (Pass3).  Verify RS(10+4)
+// 75.4-76.3 -> 79.1-81.6 %; passes that store rows do not gain (encode
+// RS(10+4) 72 % either way, the decode with checks loses 2-3 points;
+// profiles/r03_kbench_tri_{off,on}.txt).  RSGPU_TRIPLES=0 / 2 (off / every
+// pass of >= 3 rows) overrides, for measurement.
+inline bool use_triples(int K, int R, int ki, int nw) {
+    static const int env = [] {
+        const char *e = std::getenv("RSGPU_TRIPLES");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (env == 0) return false;
+    if (env == 2) return R >= 3 && K - ki >= 6;  // every pass of >= 3 rows
+    return R >= 3 && K - ki >= 6 && nw == 0;
+}
+
+// LDS reservation (occupancy cap) of a pass: store_lds(K) for passes that
+// store rows, none for check-only passes; RSGPU_MIXED_W=w overrides the cap
+// of passes that both store and check rows (measurement)
+inline unsigned pass_lds(int K, int nw, int R) {
+    if (nw == 0) return 0u;
+    static const int mixed_w = [] {
+        const char *e = std::getenv("RSGPU_MIXED_W");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (nw < R && mixed_w > 0) return mixed_w >= 8 ? 0u : 160u * 1024u / (unsigned)mixed_w - 256u;
+    // passes that store rows AND check rows (the fused decode with extra
+    // parity shards) carry the check rows' VALU work: one workgroup more per
+    // CU than store_lds gives them (RS(10+4) decode with 2 checks, K = 12:
+    // W = 4 69.7-70.2 % vs W = 3 68.7-69.0 %, W = 6 / uncapped 68.5-68.9 %;
+    // input triples on this pass lose 0.3-3 points at every W;
+    // profiles/r03_kbench_dec10_4_sweep.txt)
+    if (nw < R) return K <= 10 ? store_lds(K) : 160u * 1024u / 4u - 256u;
+    return store_lds(K);
+}
+
+template <int K, int R>
+hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
+                        hipStream_t st);
+
+// The same launch with the pass's GF inputs in triples (chunk and small-object forms)
+template <int K, int R>
+hipError_t launch_fixed3(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad, hipStream_t st);
+
 template <int K, int R>
 hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
                         hipStream_t st) {
+    if constexpr (R >= 3 && K >= 6) {
+        const int ki = (s.r0 + R == p.R) ? std::min(p.ki, R) : 0;
+        if (!L.in_base && !L.out_base && use_triples(K, R, ki, s.nw)) return launch_fixed3<K, R>(p, s, L, d_bad, st);
+    }
     ApplyArgs<K, R> a;
     a.obj_stride = L.obj_stride;
     a.nvec = (uint32_t)((L.shard_len + 15) / 16);
@@ -380,7 +452,7 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
                 // encode, 0 on decode and -7 / -4 points at 4 / 16 KiB:
                 // tools/kbench KB_SET=small, not shipped)
                 hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormSmall>),
-                                   dim3(grid), dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
+                                   dim3(grid), dim3(kBlock), pass_lds(K, (int)a.p.nw, R), st, a);
                 hipError_t e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
@@ -401,10 +473,65 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
         a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
         if (L.in_base || L.out_base)
             hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormRedirect>),
-                               dim3(grid), dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
+                               dim3(grid), dim3(kBlock), pass_lds(K, (int)a.p.nw, R), st, a);
         else
             hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormChunks>),
-                               dim3(grid), dim3(kBlock), a.p.nw ? store_lds(K) : 0u, st, a);
+                               dim3(grid), dim3(kBlock), pass_lds(K, (int)a.p.nw, R), st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+template <int K, int R>
+hipError_t launch_fixed3(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad, hipStream_t st) {
+    ApplyArgs<K, R, Pass3<K, R>> a;
+    a.obj_stride = L.obj_stride;
+    a.nvec = (uint32_t)((L.shard_len + 15) / 16);
+    a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * 16);
+    fill_pass<K, R>(p, s, L.pitch, row_space(L), a.nvec, d_bad != nullptr, a.p);
+    fill_triples<K, R>(p, s, a.p);
+    a.p.sub_stride = L.sub_stride;
+    a.p.sub_len = L.sub_len;
+    a.p.sub_n = L.sub_n;
+    a.in_base = a.out_base = nullptr;
+    a.in_span = a.copy_in = a.out_dual = 0;
+    const unsigned gx = (a.nvec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
+    a.opw = 1;
+    a.nobj = 0;
+    a.gspan = 0;
+    if (L.nobj > 1 && kUnroll == 1 && a.nvec * 2 <= kBlock) {  // small objects: as launch_fixed
+        uint32_t opw = kBlock / a.nvec;
+        while (opw > 1 && (uint64_t)(opw - 1) * L.obj_stride + a.p.span >= 0xffffffffull) opw /= 2;
+        if (opw > 1) {
+            a.opw = opw;
+            a.gspan = (uint32_t)((uint64_t)(opw - 1) * L.obj_stride + a.p.span);
+            const int groups = (L.nobj + (int)opw - 1) / (int)opw;
+            for (int g0 = 0; g0 < groups; g0 += max_items(1)) {
+                const int ng = std::min(max_items(1), groups - g0);
+                const size_t o0 = (size_t)g0 * opw;
+                a.base = L.base + o0 * L.obj_stride;
+                a.bad = d_bad ? d_bad + o0 : nullptr;
+                a.nobj = (uint32_t)std::min<size_t>((size_t)ng * opw, (size_t)L.nobj - o0);
+                unsigned grid;
+                a.ord = make_order(1, (uint32_t)ng, (size_t)a.nobj * L.obj_stride, grid);
+                hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormSmall, true>),
+                                   dim3(grid), dim3(kBlock), pass_lds(K, (int)a.p.nw, R), st, a);
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+            }
+            return hipSuccess;
+        }
+    }
+    const int step = max_items(gx);
+    for (int o0 = 0; o0 < L.nobj; o0 += step) {
+        const int no = std::min(step, L.nobj - o0);
+        a.base = L.base + (size_t)o0 * L.obj_stride;
+        a.bad = d_bad ? d_bad + o0 : nullptr;
+        unsigned grid;
+        a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.p.span), grid);
+        hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormChunks, true>),
+                           dim3(grid), dim3(kBlock), pass_lds(K, (int)a.p.nw, R), st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -926,7 +1053,7 @@ hipError_t launch_var_t(const Plan &p, const Sub &s, const VarObj *d_objs, uint3
     unsigned grid;
     a.ord = make_order(1, total, (size_t)1 << 40, grid);
     hipLaunchKernelGGL((gf_apply_var<K, R, kBlock, kLoadAux, kStoreAux>), dim3(grid), dim3(kBlock),
-                       a.p.nw ? store_lds(K) : 0u, st, a);
+                       pass_lds(K, (int)a.p.nw, R), st, a);
     return hipGetLastError();
 }
 

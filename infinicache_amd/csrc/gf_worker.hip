@@ -712,7 +712,7 @@ int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_
     if (atlas_estimate(ctx->k, ctx->p, true) > ((size_t)32 << 20)) return RSGPU_ERR_NOT_IMPLEMENTED;
     if (!nslots) nslots = 8;
     if (!idle_us) idle_us = 50000;
-    if (!max_shard) max_shard = 16384;
+    if (!max_shard) max_shard = 4096;  // worker ahead of the stream path up to ~40 KB objects (r03_lat_*_sizes.txt)
     if (max_shard > ((size_t)1 << 24)) return RSGPU_ERR_INVALID_ARG;
     DeviceGuard dg_;
     int e = ctx->use_device(dg_);

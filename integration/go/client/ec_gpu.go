@@ -128,6 +128,16 @@ func newGPUEncoder(dataShards, parityShards int) (reedsolomon.Encoder, error) {
 			return nil, errors.New(C.GoString(C.rsgpu_strerror(C.RSGPU_ERR_NO_DEVICE)))
 		}
 	}
+	// One EcSet / EcGet codes one object (ecRedis.go:96, :173): the resident
+	// worker answers those calls without a kernel launch per call
+	// (rsgpu_worker_start).  INFINICACHE_EC_WORKER=0 keeps the stream path;
+	// codes of more than 16 shards (ErrNotImplemented) keep it too.
+	if os.Getenv("INFINICACHE_EC_WORKER") != "0" {
+		if rc := C.rsgpu_worker_start(ctx, 0, 0, 0); rc != 0 && rc != C.RSGPU_ERR_NOT_IMPLEMENTED {
+			C.rsgpu_destroy(ctx)
+			return nil, rsErr(rc)
+		}
+	}
 	e := &gpuEncoder{ctx: ctx, DataShards: dataShards, ParityShards: parityShards,
 		Shards: dataShards + parityShards}
 	runtime.SetFinalizer(e, func(e *gpuEncoder) {

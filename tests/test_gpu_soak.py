@@ -13,7 +13,11 @@ than tests/test_gpu_random.py:
   * pinned Split buffers (zero-copy passes) for every per-object op;
   * round 2: narrow pitches (down to byte-packed rows), device-resolved mixed
     patterns (present masks in HBM, every status value), shard-major batches
-    (encode vs the oracle, per-object Verify flags, fused decode).
+    (encode vs the oracle, per-object Verify flags, fused decode);
+  * round 3: the resident worker (every per-object op, pinned and pageable,
+    codes of <= 16 shards, shards up to 16 KiB) and variable-size device
+    tables (rsgpu_*_dev_objs: encode, Verify flags, fused decode,
+    ReconstructData over objects of different sizes and pitches).
 Every result is compared bit-exact (bytes) or exactly (booleans, error
 classes) with the oracle on the same input.  Prints a per-kind case count."""
 import collections
@@ -347,6 +351,150 @@ def _pinned_case(rng, counts):
             assert np.array_equal(rows[i], want[i]), (tag, lost, i)
 
 
+_WORKERS = {}
+
+
+def _worker_enc(k, p, kind):
+    """one worker-enabled encoder per code (a start builds atlases and launches)"""
+    key = (k, p, kind)
+    if key not in _WORKERS:
+        if len(_WORKERS) >= 6:
+            _WORKERS.pop(next(iter(_WORKERS))).worker_stop()
+        enc = ia.New(k, p, matrix=kind)
+        enc.worker_start(nslots=4)
+        _WORKERS[key] = enc
+    return _WORKERS[key]
+
+
+def _worker_case(rng, counts):
+    k = int(rng.integers(1, 14))
+    p = int(rng.integers(1, min(5, 16 - k) + 1))
+    n = k + p
+    size = _size(rng, 16384)
+    kind = str(rng.choice(["vandermonde", "cauchy"]))
+    enc = _worker_enc(k, p, kind)
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    e, full = oracle.encode(k, p, data + [bytes(size)] * p, kind)
+    assert e == 0
+    pinned = rng.random() < 0.5
+    if pinned:
+        host = ia.host_alloc(n * size)
+        rows = [host[i * size:(i + 1) * size] for i in range(n)]
+    else:
+        rows = [np.empty(size, np.uint8) for _ in range(n)]
+    op = str(rng.choice(["encode", "encode_verify", "verify", "reconstruct", "rdata", "decode"]))
+    counts["worker_" + op] += 1
+    tag = ("worker", op, k, p, size, kind, pinned)
+    for i in range(n):
+        rows[i][:] = full[i] if i < k or op not in ("encode", "encode_verify") else 0x5C
+    if op in ("encode", "encode_verify"):
+        if op == "encode":
+            enc.Encode(rows)
+        else:
+            assert enc.EncodeVerify(rows), tag
+        for r in range(k, n):
+            assert np.array_equal(rows[r], full[r]), tag
+    elif op == "verify":
+        if rng.random() < 0.5:
+            rows[int(rng.integers(0, n))][int(rng.integers(0, size))] ^= 0x11
+        e, want = oracle.verify(k, p, [r.copy() for r in rows], kind)
+        assert e == 0 and enc.Verify(rows) == want, tag
+    else:
+        lost = sorted(rng.choice(n, int(rng.integers(1, p + 1)), replace=False).tolist())
+        if rng.random() < 0.3:
+            rows[int(rng.integers(0, n))][int(rng.integers(0, size))] ^= 0x81
+        ref = [None if i in lost else rows[i].copy() for i in range(n)]
+        e, want = oracle.reconstruct(k, p, [None if r is None else r.copy() for r in ref], kind,
+                                     data_only=(op == "rdata"))
+        assert e == 0
+        lens = [0 if i in lost else size for i in range(n)]
+        for i in lost:
+            rows[i][:] = 0xEE
+        if op == "decode":
+            ok = ctypes.c_int(7)
+            assert _call(enc, "rsgpu_decode", rows, lens, ctypes.byref(ok)) == 0, tag
+            e2, want_ok = oracle.verify(k, p, want, kind)
+            assert e2 == 0 and bool(ok.value) == want_ok, tag
+        else:
+            assert _call(enc, "rsgpu_reconstruct", rows, lens, int(op == "rdata")) == 0, tag
+        for i in range(n):
+            if op == "rdata" and i >= k and i in lost:
+                assert (rows[i] == 0xEE).all(), tag  # missing parity left alone
+                continue
+            assert np.array_equal(rows[i], want[i]), (tag, lost, i)
+
+
+def _objs_case(rng, counts):
+    """variable-size device tables: objects of different sizes and pitches,
+    one launch per pass"""
+    import torch
+    k = int(rng.integers(1, 21))
+    p = int(rng.integers(1, 7))
+    n = k + p
+    kind = str(rng.choice(["vandermonde", "cauchy"]))
+    enc = ia.New(k, p, matrix=kind)
+    m = enc.matrix()
+    nobj = int(rng.integers(1, 40))
+    layout, off = [], 0
+    for _ in range(nobj):
+        S = _size(rng, 60000)
+        pitch = (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+        layout.append((off, S, pitch))
+        off += n * pitch + 16 * int(rng.integers(0, 4))
+    host = rng.integers(0, 256, off + 64, dtype=np.uint8)
+    buf = torch.from_numpy(host.copy()).cuda()
+    objs = [(buf.data_ptr() + o, S, pitch) for o, S, pitch in layout]
+    st = torch.cuda.current_stream()
+    tag = ("objs", k, p, nobj, kind)
+    enc.encode_dev_objs(objs, st)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    rows = lambda a, o, S, pitch: [a[o + i * pitch: o + i * pitch + S] for i in range(n)]
+    for o, S, pitch in layout:
+        r = rows(got, o, S, pitch)
+        want = oracle.apply(m[k:], [h.copy() for h in rows(host, o, S, pitch)[:k]])
+        for j in range(p):
+            assert np.array_equal(r[k + j], want[j]), (tag, S)
+    counts["objs_encode"] += 1
+    coded = got.copy()
+    op = str(rng.choice(["verify", "decode", "rdata"]))
+    counts["objs_" + op] += 1
+    bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    if op == "verify":
+        hit = sorted(set(rng.integers(0, nobj, int(rng.integers(0, min(nobj, 5) + 1))).tolist()))
+        for i in hit:
+            o, S, pitch = layout[i]
+            got[o + int(rng.integers(0, n)) * pitch + int(rng.integers(0, S))] ^= 0x33
+        buf = torch.from_numpy(got).cuda()
+        objs = [(buf.data_ptr() + o, S, pitch) for o, S, pitch in layout]
+        enc.verify_dev_objs(objs, bad, st)
+        torch.cuda.synchronize()
+        assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit, tag
+        return
+    lost = sorted(rng.choice(n, int(rng.integers(1, p + 1)), replace=False).tolist())
+    for o, S, pitch in layout:
+        for i in lost:
+            got[o + i * pitch: o + i * pitch + S] = 0xA5
+    buf = torch.from_numpy(got.copy()).cuda()
+    objs = [(buf.data_ptr() + o, S, pitch) for o, S, pitch in layout]
+    present = [i not in lost for i in range(n)]
+    if op == "decode":
+        enc.decode_dev_objs(objs, present, bad, st)
+    else:
+        enc.reconstruct_dev_objs(objs, present, data_only=True, stream=st)
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    if op == "decode":
+        assert not bad.any(), tag
+    for o, S, pitch in layout:
+        for i in range(n):
+            a = out[o + i * pitch: o + i * pitch + S]
+            if op == "rdata" and i >= k and i in lost:
+                assert (a == 0xA5).all(), tag
+            else:
+                assert np.array_equal(a, coded[o + i * pitch: o + i * pitch + S]), (tag, op, lost, i)
+
+
 def test_gpu_soak_vs_oracle(gpu):
     seed = int(os.environ.get("RSGPU_SOAK_SEED", "20261016"))
     rng = np.random.default_rng(seed)
@@ -354,19 +502,26 @@ def test_gpu_soak_vs_oracle(gpu):
     t0 = last = time.time()
     while time.time() - t0 < SECONDS:
         r = rng.random()
-        if r < 0.3:
+        if r < 0.22:
             _host_case(rng, counts)
-        elif r < 0.55:
+        elif r < 0.42:
             _device_case(rng, counts)
-        elif r < 0.7:
+        elif r < 0.54:
             _masks_case(rng, counts)
-        elif r < 0.85:
+        elif r < 0.66:
             _shard_major_case(rng, counts)
-        else:
+        elif r < 0.76:
             _pinned_case(rng, counts)
+        elif r < 0.9:
+            _worker_case(rng, counts)
+        else:
+            _objs_case(rng, counts)
         if time.time() - last > 30:  # progress line (a silent GPU run reads as hung)
             last = time.time()
             print(f"soak {last - t0:.0f}s: {sum(counts.values())} cases", flush=True)
+    for enc in _WORKERS.values():
+        enc.worker_stop()
+    _WORKERS.clear()
     print(f"soak seed {seed}, {time.time() - t0:.0f} s, {sum(counts.values())} cases:", flush=True)
     for key in sorted(counts):
         print(f"  {key:22s} {counts[key]}", flush=True)
