@@ -42,7 +42,7 @@ def test_worker_every_op_vs_oracle(gpu, pinned):
     k, p = 10, 2
     n = k + p
     enc = ia.New(k, p)
-    enc.worker_start()
+    enc.worker_start(max_shard=16384)
     for idx, S in enumerate([1, 15, 16, 17, 103, 410, 1000, 4096, 4099, 16384]):
         full = _full(k, p, S, idx)
         buf, sh = _image(n, S, pinned)
@@ -89,7 +89,7 @@ def test_worker_in_place_pinned_image_missing_rows(gpu):
     k, p = 10, 2
     n = k + p
     enc = ia.New(k, p)
-    enc.worker_start()
+    enc.worker_start(max_shard=8192)
     L = ia._lib.load()
     import ctypes
     for idx, S in enumerate([103, 2048, 5003]):
