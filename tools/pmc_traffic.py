@@ -21,9 +21,11 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"(gf_apply_kernel|gf_apply_generic)<([^>]*)>", name)
+    m = re.search(r"(gf_\w+)(?:<([^>]*)>)?", name)
     if not m:
         return name[:80]
+    if m.group(2) is None:
+        return m.group(1)
     args = [a.strip() for a in m.group(2).split(",")]
     return f"{m.group(1)}<{','.join(args[:2])}>" if m.group(1) == "gf_apply_kernel" else f"{m.group(1)}<{args[0]}>"
 
@@ -58,7 +60,7 @@ def main():
             dur[short(row["Name"])] = float(row["AverageNs"])
     res = {}
     for k in fetch:
-        if not k.startswith("gf_apply"):
+        if not k.startswith("gf_"):
             continue
         fkib, n = fetch[k]
         wkib = write.get(k, (0.0, 0))[0]
