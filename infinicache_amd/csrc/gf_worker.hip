@@ -49,6 +49,32 @@ __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_re
 constexpr uint32_t kLaneVecs = 64;  // lane-parallel path: vectors per pass at most
 constexpr uint32_t kLaneU = 4;      // ... and passes (their loads issued up front)
 
+// Encode+Verify's check of a parity vector as stored in host memory: the
+// read is issued right behind the store, so the store's completion and the
+// read's PCIe round trip overlap (r03: the read waited for the store before,
+// 1.3 us + 1.8 us).  Both go to the same address with system-coherent
+// policy, and a PCIe read does not pass the posted writes before it, so the
+// read should see the new bytes; should it ever see old ones, the wave waits
+// for every store to complete and reads again, so only a mismatch that
+// survives the second read is reported.  `valid`: bytes of the vector
+// compared (0: none).
+__device__ __forceinline__ bool readback_check(const u32x4 &want, __amdgpu_buffer_rsrc_t rs, uint32_t voff,
+                                               uint32_t soff, uint32_t valid) {
+    asm volatile("" ::: "memory");  // the load stays behind the store in program order
+    u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, kSysAux);
+    bool mm = false;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) mm |= ((b[d] ^ want[d]) & tail_mask(d, valid)) != 0;
+    if (__builtin_amdgcn_ballot_w64(mm) != 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        b = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, kSysAux);
+        mm = false;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) mm |= ((b[d] ^ want[d]) & tail_mask(d, valid)) != 0;
+    }
+    return mm;
+}
+
 // the c-th set bit of m (per lane; m < 2^16)
 __device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t c) {
 #pragma unroll
@@ -254,14 +280,11 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
                             const uint32_t row = (orow >> (8 * r)) & 0xffu;
                             store_row<kSysAux>(acc, rso, v * 16u, row * pitch, v == nvec - 1 ? part : 0u);
                             if (op == kWopEncodeVerify) {
-                                // Verify on the parity rows as stored: the store
-                                // completes, then the row is read back over PCIe
-                                // (a read does not pass the posted writes before it)
-                                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                // Verify on the parity row as stored: read it back over
+                                // PCIe (readback_check: issued behind the store, confirmed
+                                // after the stores complete on a mismatch)
                                 if (a.trace && u == 0 && s == 0 && t == 0) t3 = __builtin_amdgcn_s_memrealtime();
-                                const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rso, v * 16u, row * pitch, kSysAux);
-#pragma unroll
-                                for (int d = 0; d < 4; ++d) mismatch |= ((b[d] ^ acc[d]) & tail_mask(d, valid)) != 0;
+                                mismatch |= readback_check(acc, rso, v * 16u, row * pitch, valid);
                                 if (a.trace && u == 0 && s == 0 && t == 0) t4 = __builtin_amdgcn_s_memrealtime();
                             }
                         } else {
@@ -328,16 +351,13 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
                     }
                 }
                 if (op == kWopEncodeVerify && nw > 0) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (a.trace && c0 == 0 && s == 0) t3 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
                     for (int r = 0; r < RM; ++r) {
                         if ((uint32_t)r >= nw) continue;
                         const uint32_t row = (orow >> (8 * r)) & 0xffu;
-                        const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rso, voff, row * pitch, kSysAux);
-                        if (live)
-#pragma unroll
-                            for (int d = 0; d < 4; ++d) mismatch |= ((b[d] ^ acc[r][d]) & tail_mask(d, valid)) != 0;
+                        const u32x4 o = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+                        mismatch |= readback_check(o, rso, voff, row * pitch, live ? valid : 0u);
                     }
                     if (a.trace && c0 == 0 && s == 0) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
