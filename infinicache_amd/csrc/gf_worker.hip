@@ -9,7 +9,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <set>
 #include <thread>
 
 #include "ctx.h"
@@ -715,6 +717,32 @@ int worker_stop(rsgpu_ctx *ctx) {
 
 }  // namespace rsgpu
 
+// Contexts with a worker, for the process-exit guard: a resident kernel
+// still polling when the HIP runtime tears down would read freed pinned
+// mailboxes (a GPU memory fault), and a Go or C host that exits without
+// rsgpu_destroy is normal.  The guard is registered with atexit after the
+// HIP runtime has initialised (its own teardown was registered before), so
+// it runs first and stops every worker.
+namespace {
+std::mutex g_live_mu;
+std::set<rsgpu_ctx *> g_live;
+void stop_all_workers() {
+    std::vector<rsgpu_ctx *> live;
+    {
+        std::lock_guard<std::mutex> l(g_live_mu);
+        live.assign(g_live.begin(), g_live.end());
+    }
+    for (rsgpu_ctx *c : live) (void)rsgpu_worker_stop(c);
+}
+void track_worker(rsgpu_ctx *ctx, bool on) {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(stop_all_workers); });
+    std::lock_guard<std::mutex> l(g_live_mu);
+    if (on) g_live.insert(ctx);
+    else g_live.erase(ctx);
+}
+}  // namespace
+
 // ============================================================== C ABI
 
 extern "C" {
@@ -745,6 +773,7 @@ int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_
     std::unique_ptr<Worker> w;
     if ((e = worker_create(ctx, nslots, idle_us, max_shard, w))) return e;
     ctx->worker.reset(w.release());
+    track_worker(ctx, true);
     return RSGPU_OK;
 }
 
@@ -777,11 +806,15 @@ int rsgpu_worker_stop(rsgpu_ctx *ctx) {
         return first;
     }
     std::lock_guard<std::mutex> l(ctx->worker_mu);
-    if (!ctx->worker) return RSGPU_OK;
+    if (!ctx->worker) {
+        track_worker(ctx, false);  // (a restart whose create failed left it listed)
+        return RSGPU_OK;
+    }
     DeviceGuard dg_;
     int e = ctx->use_device(dg_);
     if (!e) e = worker_stop(ctx);
     ctx->worker.reset();
+    track_worker(ctx, false);
     return e;
 }
 

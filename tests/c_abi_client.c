@@ -270,7 +270,38 @@ static int ecredis_replay(size_t N, int worker) {
     return 0;
 }
 
+/* A host that exits with the resident worker still running and without
+ * rsgpu_destroy (a Go client process simply ends): the library's exit guard
+ * must stop the worker before the HIP runtime tears down.  With
+ * RSGPU_WORKER_TRACE set, worker_stop's trace line on stderr shows that it
+ * ran at exit. */
+static int exit_with_worker(void) {
+    const int k = 10, n = 12;
+    const size_t S = 103;
+    rsgpu_ctx *ctx = NULL;
+    CHECK(rsgpu_create(k, 2, 0, 0, &ctx) == RSGPU_OK);
+    CHECK(rsgpu_worker_start(ctx, 2, 10000000u, 0) == RSGPU_OK); /* 10 s idle: running at exit */
+    uint8_t *buf[12], *ref[12];
+    size_t lens[12];
+    for (int i = 0; i < n; i++) {
+        buf[i] = calloc(S, 1);
+        ref[i] = calloc(S, 1);
+        lens[i] = S;
+        for (size_t j = 0; i < k && j < S; j++) buf[i][j] = ref[i][j] = rnd8();
+    }
+    int ok = 0;
+    CHECK(rsgpu_encode_verify(ctx, buf, lens, n, &ok) == RSGPU_OK && ok == 1);
+    CHECK(orc_encode(k, 2, 0, ref, lens, n) == 0);
+    for (int i = 0; i < n; i++) CHECK(memcmp(buf[i], ref[i], S) == 0);
+    uint64_t served = 0;
+    CHECK(rsgpu_worker_stats(ctx, &served, NULL, NULL) == RSGPU_OK && served == 1);
+    printf("exit with the worker running\n");
+    fflush(stdout);
+    return 0; /* no rsgpu_worker_stop, no rsgpu_destroy */
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && strcmp(argv[1], "exit_with_worker") == 0) return exit_with_worker();
     if (host_checks()) return 1;
     if (argc > 1 && strcmp(argv[1], "gpu") == 0)
         return gpu_checks() || ecredis_replay(1 << 20, 0) || ecredis_replay(1024, 1);

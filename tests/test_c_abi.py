@@ -39,3 +39,15 @@ def test_c_abi_gpu_paths(gpu, client_bin):
     assert r.returncode == 0, r.stderr + r.stdout
     assert "gpu checks ok" in r.stdout
     assert "ecredis replay ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_c_abi_exit_with_worker_running(gpu, client_bin):
+    """A process that ends with the resident kernel still polling and no
+    rsgpu_destroy (a Go client just exits): the library's atexit guard stops
+    the worker before the runtime frees its mailboxes."""
+    env = dict(os.environ, RSGPU_WORKER_TRACE="1")
+    r = subprocess.run([client_bin, "exit_with_worker"], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "exit with the worker running" in r.stdout
+    assert "rsgpu worker trace encode+verify" in r.stderr, r.stderr
