@@ -12,6 +12,7 @@
 // operation.
 #pragma once
 #include <array>
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <mutex>
@@ -38,13 +39,14 @@ struct Plan {
     std::vector<uint8_t> coef;   // R x K
     std::vector<uint32_t> tab;   // [R][K][kCoefWords] kernel tables
     int ki = 0;                  // trailing identity inputs (gf_apply_kernel)
-    // device copies for the generic (K > 16) kernel; uploaded once, then
-    // immutable (safe for concurrent launches)
+    // device copies for the generic (K > 16) kernel; uploaded by the first
+    // launch that succeeds, then immutable (safe for concurrent launches).  A
+    // failed upload frees what it allocated and the next launch retries.
     uint32_t *d_tab = nullptr;     // [K][R][kCoefWords] (input-major)
     uint32_t *d_in_row = nullptr;  // [K]
     uint32_t *d_tab3 = nullptr;    // [K/3][R][16] input-triple tables (gf_apply_generic)
-    std::once_flag dev_once;
-    hipError_t dev_err = hipSuccess;
+    std::mutex dev_mu;
+    std::atomic<bool> dev_done{false};
     // serialized Pass images for mixed-pattern launches, keyed by (pitch and
     // flags, first row, vectors per row): the image's span depends on all three
     std::mutex img_mu;

@@ -689,51 +689,70 @@ stage_fn pick_stage(int K, int R) {
     }
 }
 
+// Uploads the generic kernel's [K][R][kTabWords] table image, its triple
+// tables and row indices (Plan::d_*); on failure frees what it allocated.
+static hipError_t upload_generic(Plan &p) {
+    const int K = p.K;
+    // rows padded: the pipelined loads reach up to 3 rows past the last
+    // triple (through a zero-record resource)
+    std::vector<uint32_t> t((size_t)K * p.R * kTabWords), rows(K + kRowPad, 0);
+    for (int c = 0; c < K; ++c) {
+        rows[c] = (uint32_t)p.in_rows[c];
+        for (int r = 0; r < p.R; ++r)
+            for (int g = 0; g < kTabWords; ++g)
+                t[((size_t)c * p.R + r) * kTabWords + g] = p.tab[((size_t)r * K + c) * kTabWords + g];
+    }
+    // input-triple tables [K/3][R][16]: words 0-7 the low halves (entries
+    // 0-3) of the eight 8-entry tables, words 8-15 their high halves
+    const GF &gf_ = gf();
+    const int nt = K / 3;
+    std::vector<uint32_t> t3((size_t)std::max(1, nt) * p.R * 16, 0);
+    for (int tr = 0; tr < nt; ++tr)
+        for (int r = 0; r < p.R; ++r) {
+            const uint8_t ca = p.coef[(size_t)r * K + 3 * tr], cb = p.coef[(size_t)r * K + 3 * tr + 1],
+                          cc = p.coef[(size_t)r * K + 3 * tr + 2];
+            uint32_t *w = &t3[((size_t)tr * p.R + r) * 16];
+            for (int j = 0; j < 8; ++j) {
+                const uint8_t ent[8] = {
+                    gf_.mul(ca, (uint8_t)j), gf_.mul(ca, (uint8_t)(j << 3)),
+                    gf_.mul(cb, (uint8_t)j), gf_.mul(cb, (uint8_t)(j << 3)),
+                    gf_.mul(cc, (uint8_t)j), gf_.mul(cc, (uint8_t)(j << 3)),
+                    (uint8_t)(gf_.mul(ca, (uint8_t)((j >> 1) << 6)) ^ gf_.mul(cb, (uint8_t)((j & 1) << 7))),
+                    (uint8_t)(gf_.mul(cb, (uint8_t)((j & 1) << 6)) ^ gf_.mul(cc, (uint8_t)((j >> 1) << 6)))};
+                for (int g = 0; g < 8; ++g) w[g + (j >> 2) * 8] |= (uint32_t)ent[g] << (8 * (j & 3));
+            }
+        }
+    hipError_t e = hipMalloc(&p.d_tab, t.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&p.d_tab3, t3.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(p.d_tab3, t3.data(), t3.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p.d_in_row, rows.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(p.d_tab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p.d_in_row, rows.data(), rows.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        for (uint32_t **d : {&p.d_tab, &p.d_tab3, &p.d_in_row}) {
+            if (*d) (void)hipFree(*d);
+            *d = nullptr;
+        }
+        return e;
+    }
+    return hipSuccess;
+}
+
 template <int R>
 hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
                           hipStream_t st) {
     const int K = p.K;
-    // upload the [K][R][kTabWords] table image and row indices once per plan
-    hipError_t e = hipSuccess;
-    std::call_once(p.dev_once, [&] {
-        // rows padded: the pipelined loads reach up to 3 rows past the last
-        // triple (through a zero-record resource)
-        std::vector<uint32_t> t((size_t)K * p.R * kTabWords), rows(K + kRowPad, 0);
-        for (int c = 0; c < K; ++c) {
-            rows[c] = (uint32_t)p.in_rows[c];
-            for (int r = 0; r < p.R; ++r)
-                for (int g = 0; g < kTabWords; ++g)
-                    t[((size_t)c * p.R + r) * kTabWords + g] = p.tab[((size_t)r * K + c) * kTabWords + g];
+    // upload once per plan (a failed upload is freed and retried by the next
+    // launch: one transient hipMalloc failure must not disable the plan for
+    // the context's life)
+    if (!p.dev_done.load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> g(p.dev_mu);
+        if (!p.dev_done.load(std::memory_order_relaxed)) {
+            const hipError_t e = upload_generic(p);
+            if (e != hipSuccess) return e;
+            p.dev_done.store(true, std::memory_order_release);
         }
-        // input-triple tables [K/3][R][16]: words 0-7 the low halves (entries
-        // 0-3) of the eight 8-entry tables, words 8-15 their high halves
-        const GF &gf_ = gf();
-        const int nt = K / 3;
-        std::vector<uint32_t> t3((size_t)std::max(1, nt) * p.R * 16, 0);
-        for (int tr = 0; tr < nt; ++tr)
-            for (int r = 0; r < p.R; ++r) {
-                const uint8_t ca = p.coef[(size_t)r * K + 3 * tr], cb = p.coef[(size_t)r * K + 3 * tr + 1],
-                              cc = p.coef[(size_t)r * K + 3 * tr + 2];
-                uint32_t *w = &t3[((size_t)tr * p.R + r) * 16];
-                for (int j = 0; j < 8; ++j) {
-                    const uint8_t ent[8] = {
-                        gf_.mul(ca, (uint8_t)j), gf_.mul(ca, (uint8_t)(j << 3)),
-                        gf_.mul(cb, (uint8_t)j), gf_.mul(cb, (uint8_t)(j << 3)),
-                        gf_.mul(cc, (uint8_t)j), gf_.mul(cc, (uint8_t)(j << 3)),
-                        (uint8_t)(gf_.mul(ca, (uint8_t)((j >> 1) << 6)) ^ gf_.mul(cb, (uint8_t)((j & 1) << 7))),
-                        (uint8_t)(gf_.mul(cb, (uint8_t)((j & 1) << 6)) ^ gf_.mul(cc, (uint8_t)((j >> 1) << 6)))};
-                    for (int g = 0; g < 8; ++g) w[g + (j >> 2) * 8] |= (uint32_t)ent[g] << (8 * (j & 3));
-                }
-            }
-        e = hipMalloc(&p.d_tab, t.size() * 4);
-        if (e == hipSuccess) e = hipMalloc(&p.d_tab3, t3.size() * 4);
-        if (e == hipSuccess) e = hipMemcpy(p.d_tab3, t3.data(), t3.size() * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMalloc(&p.d_in_row, rows.size() * 4);
-        if (e == hipSuccess) e = hipMemcpy(p.d_tab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(p.d_in_row, rows.data(), rows.size() * 4, hipMemcpyHostToDevice);
-        p.dev_err = e;
-    });
-    if (p.dev_err != hipSuccess) return p.dev_err;
+    }
     // 8-B lane vectors for narrow passes that write rows: 51 VGPRs at R = 4
     // (8 waves) against 81 (5 waves); RS(20+4) encode +2.5, RS(17+3) +3
     // points, the wide encode+decode workload +3 %.  Wider passes and
