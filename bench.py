@@ -276,6 +276,18 @@ class DistCtx:
         dist.all_reduce(t)
         return int(t.item())
 
+    def gather(self, x: float) -> list:
+        """Every rank's value of x, in rank order (a SUM-reduce of one-hot
+        vectors: the same collective as the barrier, no payload besides)."""
+        if self.world == 1:
+            return [x]
+        import torch
+        import torch.distributed as dist
+        t = torch.zeros(self.world, dtype=torch.float64, device=self.device)
+        t[self.rank] = x
+        dist.all_reduce(t)
+        return [float(v) for v in t.cpu()]
+
 
 def shard_objects(nobj_total: int, rank: int, world: int):
     """Contiguous object range of `rank` for strong scaling (objects are
@@ -834,6 +846,8 @@ def main():
     dom_ms = float(np.mean([m for _, m in members]))
     dom = "+".join(op for op, _ in members)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    # every rank's own kernel rate (N > 1: each GPU codes its own objects)
+    frac_ranks = [round(a / HBM_PEAK_GBS, 4) for a in dctx.gather(achieved)]
     traffic = pmc_traffic(kernel_key, args.workload, dom_bytes)
     roofline = {
         "bound": "hbm",
@@ -851,6 +865,9 @@ def main():
         # the read side alone (k*S input bytes per object and launch), SURVEY §8d
         "read_only": {"achieved": round(nobj * k * S / (dom_ms * 1e-3) / 1e9, 1),
                       "frac": round(nobj * k * S / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        # achieved / peak of the same kernel on each rank's GPU (rank order);
+        # achieved and frac above are rank 0's
+        "frac_per_rank": frac_ranks,
     }
 
     warm = None

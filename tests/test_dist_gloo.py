@@ -46,10 +46,11 @@ def _worker(rank, world, port, nobj_total, q):
 
         el = bench.timed_run(step, steps=2, warmup=1, sync=lambda: None, dctx=dctx)
         total = dctx.sum(count)
+        gathered = dctx.gather(float(rank) + 0.5)  # per-rank roofline fractions (bench.py)
         x = 0
         for d in digests:
             x ^= d
-        q.put((rank, el, total, start, count, x))
+        q.put((rank, el, total, start, count, x, gathered))
     finally:
         dist.destroy_process_group()
 
@@ -72,6 +73,7 @@ def test_gloo_object_per_rank(world):
     assert len(els) == 1                       # every rank reports the same MAX
     assert min(els) >= 2 * 0.05 * world         # >= the slowest rank's two steps
     assert all(r[2] == nobj for r in res)       # all objects accounted exactly once
+    assert all(r[6] == [i + 0.5 for i in range(world)] for r in res)  # gather: rank order
     spans = [(r[3], r[4]) for r in res]
     assert spans[0][0] == 0 and sum(c for _, c in spans) == nobj
     assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
