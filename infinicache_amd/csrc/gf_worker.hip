@@ -589,6 +589,15 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
     const uint32_t n = ++w.seq[i];
     for (int g = 0; g < 8; ++g)
         __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)n << 32), __ATOMIC_RELEASE);
+    // a call that fails takes its request back (tags of the last number
+    // served, which no workgroup accepts) and rewinds the slot's count: the
+    // caller's buffers may be gone by the time a later launch polls the slot
+    auto retract = [&](int err) {
+        for (int g = 0; g < 8; ++g)
+            __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)(n - 1) << 32), __ATOMIC_RELEASE);
+        --w.seq[i];
+        return err;
+    };
     uint32_t cur = w.gen.load(std::memory_order_acquire);
     const auto t_post = std::chrono::steady_clock::now();
     unsigned spins = 0;
@@ -610,8 +619,10 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
             // launched): the request line stays posted, a new launch serves it
             std::lock_guard<std::mutex> l(w.mu);
             if (w.gen.load() == cur) {
-                HIP_TRY(hipStreamSynchronize(w.stream));  // every workgroup of `cur` leaves promptly
-                HIP_TRY(launch(w, cur + 1));
+                // every workgroup of `cur` leaves promptly
+                hipError_t he = hipStreamSynchronize(w.stream);
+                if (he != hipSuccess) return retract(hip_fail(he, "resident worker"));
+                if ((he = launch(w, cur + 1)) != hipSuccess) return retract(hip_fail(he, "resident worker launch"));
                 w.gen.store(cur + 1, std::memory_order_release);
                 w.launches.fetch_add(1, std::memory_order_relaxed);
             }
@@ -620,7 +631,7 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
         }
         if ((++spins & 0xfffffu) == 0) {  // a kernel that died without answering
             const hipError_t q = hipStreamQuery(w.stream);
-            if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "resident worker");
+            if (q != hipSuccess && q != hipErrorNotReady) return retract(hip_fail(q, "resident worker"));
         }
     }
 }
