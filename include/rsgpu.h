@@ -256,8 +256,12 @@ int rsgpu_decode_dev_multi(rsgpu_ctx *ctx, void *d_base, const uint8_t *present,
  * (bits >= data+parity ignored).  The pattern -> coefficient resolution runs
  * on the device against a per-context atlas of every erasure pattern, built
  * and uploaded on the first call: no per-call host planning, upload or host
- * synchronisation.  Requires data+parity <= 16 (else RSGPU_ERR_NOT_IMPLEMENTED;
- * the host-flag *_dev_multi calls cover wider codes).
+ * synchronisation.  Codes of 17-32 shards (and codes whose atlas would pass
+ * its size bound, e.g. data 2 + parity 14) have no atlas: the masks are read
+ * back (one synchronisation of `stream`), grouped by pattern on the host and
+ * coded by the host-planned mixed-pattern launches, with the same statuses.
+ * More than 32 shards: RSGPU_ERR_NOT_IMPLEMENTED (masks are 32-bit words; the
+ * host-flag *_dev_multi calls cover those codes).
  * d_status[o] (device uint32; optional for reconstruct) receives, per object:
  *   0  done (decode: upstream's Verify-after-Reconstruct would pass),
  *   1  decode only: that Verify would fail (ecRedis.go:420-426),

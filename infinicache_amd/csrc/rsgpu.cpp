@@ -526,20 +526,78 @@ int run_masked(rsgpu_ctx *ctx, const AtlasView &A, AtlasMode mode, const Layout 
     return RSGPU_OK;
 }
 
+// *_dev_masks for codes without a device atlas (17-32 shards, or an atlas
+// past its size bound, e.g. RS(2+14)): the masks come to the host (one
+// stream synchronisation), objects are grouped by pattern with the same
+// per-object statuses as the atlas (too few shards 2, singular 3, untouched),
+// and the groups are coded by the host-planned mixed-pattern launches.
+int dev_masks_host(rsgpu_ctx *ctx, const Layout &L, const uint32_t *d_masks, AtlasMode mode, uint32_t *d_status,
+                   hipStream_t st) {
+    const int n = ctx->n, nobj = L.nobj;
+    const uint32_t nmask = n >= 32 ? ~0u : ((1u << n) - 1);
+    std::vector<uint32_t> masks((size_t)nobj), status((size_t)nobj, kStatusOk);
+    HIP_TRY(hipMemcpyAsync(masks.data(), d_masks, (size_t)nobj * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const bool check = mode == kAtlasDecode, data_only = mode == kAtlasData;
+    std::unordered_map<uint32_t, int> slot_of;  // pattern -> plan index, or -1 - status
+    std::vector<std::shared_ptr<Plan>> owned;
+    std::vector<Plan *> plans;
+    std::vector<int> plan_of((size_t)nobj, -1);
+    std::vector<uint8_t> pr((size_t)n);
+    for (int o = 0; o < nobj; ++o) {
+        const uint32_t m = masks[o] & nmask;
+        auto ins = slot_of.emplace(m, 0);
+        if (ins.second) {  // first object with this pattern
+            const int np = __builtin_popcount(m);
+            int slot = -1 - (int)kStatusOk;
+            if (np < ctx->k) {
+                slot = -1 - (int)kStatusTooFew;
+            } else if (np < n || check) {
+                for (int i = 0; i < n; ++i) pr[i] = (uint8_t)((m >> i) & 1u);
+                std::shared_ptr<Plan> p;
+                int e = np == n ? (p = ctx->plan_verify(), RSGPU_OK) : ctx->plan_reconstruct(pr.data(), data_only, check, p);
+                if (e == RSGPU_ERR_SINGULAR) {
+                    slot = -1 - (int)kStatusSingular;
+                } else if (e) {
+                    return e;
+                } else if (p->R > 0) {
+                    slot = (int)plans.size();
+                    owned.push_back(p);
+                    plans.push_back(p.get());
+                }
+            }
+            ins.first->second = slot;
+        }
+        const int s = ins.first->second;
+        if (s >= 0) plan_of[o] = s;
+        else status[o] = (uint32_t)(-1 - s);
+    }
+    // statuses of the objects no launch touches; the coded ones start at 0
+    // and the check rows raise theirs to 1
+    if (d_status) HIP_TRY(hipMemcpy(d_status, status.data(), (size_t)nobj * 4, hipMemcpyHostToDevice));
+    if (plans.empty()) return RSGPU_OK;
+    HIP_TRY(launch_plans_multi(plans, plan_of, L, check ? d_status : nullptr, st, ctx->multi_ws));
+    return RSGPU_OK;
+}
+
 int dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_masks, size_t shard_len, size_t pitch,
               size_t obj_stride, int nobj, AtlasMode mode, uint32_t *d_status, void *stream) {
     if (!ctx || (nobj > 0 && !d_masks)) return RSGPU_ERR_INVALID_ARG;
     int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
     if (e) return e;
     if (((uintptr_t)d_base & 15) || (pitch & 15) || (obj_stride & 15)) return RSGPU_ERR_INVALID_ARG;
-    if (ctx->n > kAtlasMaxN) return RSGPU_ERR_NOT_IMPLEMENTED;
+    if (ctx->n > 32) return RSGPU_ERR_NOT_IMPLEMENTED;  // masks are 32-bit words
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
     if (nobj == 0) return RSGPU_OK;
-    AtlasView A;
-    if ((e = ctx->atlas_view(mode, A))) return e;
     Layout L{(uint8_t *)d_base, obj_stride, pitch, shard_len, nobj};
-    return run_masked(ctx, A, mode, L, d_masks, d_status, (hipStream_t)stream);
+    AtlasView A;
+    if (ctx->n <= kAtlasMaxN) {
+        e = ctx->atlas_view(mode, A);
+        if (e == RSGPU_OK) return run_masked(ctx, A, mode, L, d_masks, d_status, (hipStream_t)stream);
+        if (e != RSGPU_ERR_NOT_IMPLEMENTED) return e;
+    }
+    return dev_masks_host(ctx, L, d_masks, mode, d_status, (hipStream_t)stream);
 }
 
 }  // namespace

@@ -60,7 +60,11 @@ def _random_patterns(rng, nobj, k, p, corrupt_every=7, too_few_every=0):
 @pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 104858, 40), (10, 2, 50001, 300), (10, 4, 7777, 120),
                                         (10, 2, 103, 2000), (10, 4, 410, 700), (12, 4, 2048, 90),
                                         (4, 2, 1, 300), (10, 2, 2049, 33), (6, 6, 3000, 64),
-                                        (8, 8, 100, 257), (1, 1, 17, 40), (15, 1, 4096, 20)])
+                                        (8, 8, 100, 257), (1, 1, 17, 40), (15, 1, 4096, 20),
+                                        # no device atlas: 17-32 shards, or RS(2+14) past the atlas
+                                        # bound (masks read back, host-planned launches)
+                                        (20, 4, 3000, 50), (17, 3, 500, 100), (24, 8, 1000, 40),
+                                        (2, 14, 200, 64), (28, 4, 700, 30)])
 def test_decode_masks_random_patterns(gpu, k, p, S, nobj):
     n = k + p
     pitch = _pitch(S)
@@ -117,7 +121,9 @@ def test_decode_masks_random_patterns(gpu, k, p, S, nobj):
 
 @pytest.mark.parametrize("k,p,S,nobj,data_only", [(10, 4, 9000, 64, True), (10, 4, 9000, 64, False),
                                                   (10, 4, 300, 500, True), (10, 2, 1000, 300, False),
-                                                  (6, 6, 5000, 50, False), (6, 6, 60, 400, True)])
+                                                  (6, 6, 5000, 50, False), (6, 6, 60, 400, True),
+                                                  (20, 4, 2000, 60, True), (20, 4, 2000, 60, False),
+                                                  (4, 12, 500, 80, False)])
 def test_reconstruct_masks(gpu, k, p, S, nobj, data_only):
     n = k + p
     pitch = _pitch(S)
@@ -304,10 +310,12 @@ def test_host_flags_large_atlas_codes(gpu, k, p):
         assert torch.equal(b[o, :k, :S], golden[o, :k, :S]), o
 
 
-def test_masks_wide_code_not_implemented(gpu):
-    enc = ia.New(20, 4)
-    b = torch.zeros((2, 24, 256), dtype=torch.uint8, device="cuda")
+def test_masks_code_beyond_mask_width_not_implemented(gpu):
+    """Masks are 32-bit words: codes of more than 32 shards return
+    ErrNotImplemented (the host-flag *_dev_multi calls cover them)."""
+    enc = ia.New(30, 4)
+    b = torch.zeros((2, 34, 256), dtype=torch.uint8, device="cuda")
     m = torch.zeros(2, dtype=torch.int32, device="cuda")
     st = torch.zeros(2, dtype=torch.int32, device="cuda")
     with pytest.raises(ia.ErrNotImplemented):
-        enc.decode_dev_masks(b, m, 200, 256, 24 * 256, 2, st, torch.cuda.current_stream())
+        enc.decode_dev_masks(b, m, 200, 256, 34 * 256, 2, st, torch.cuda.current_stream())

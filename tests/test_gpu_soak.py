@@ -17,7 +17,8 @@ than tests/test_gpu_random.py:
   * round 3: the resident worker (every per-object op, pinned and pageable,
     codes of <= 16 shards, shards up to 16 KiB) and variable-size device
     tables (rsgpu_*_dev_objs: encode, Verify flags, fused decode,
-    ReconstructData over objects of different sizes and pitches).
+    ReconstructData over objects of different sizes and pitches); device
+    masks of 17-32-shard codes (no atlas: masks read back, host-planned).
 Every result is compared bit-exact (bytes) or exactly (booleans, error
 classes) with the oracle on the same input.  Prints a per-kind case count."""
 import collections
@@ -186,6 +187,9 @@ def _masks_case(rng, counts):
     import torch
     k = int(rng.integers(1, 15))
     p = int(rng.integers(1, min(8, 16 - k) + 1))
+    if rng.random() < 0.25:  # 17-32 shards: no device atlas (masks read back, host-planned)
+        k = int(rng.integers(10, 29))
+        p = int(rng.integers(max(1, 17 - k), min(8, 32 - k) + 1))
     n = k + p
     S = _size(rng, 30000)
     pitch = (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 2))
