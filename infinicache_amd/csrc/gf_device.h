@@ -403,25 +403,32 @@ static_assert(sizeof(VarObj) == 32, "VarObj: one 32-B table entry");
 template <int K, int R>
 struct VarArgs {  // one pass over objects of different sizes and pitches (kernarg)
     const VarObj *objs;
+    const uint32_t *chunk_obj;  // [total]: the object of each flattened chunk, or nullptr
     uint32_t nobj;
     uint32_t *bad;   // per object (index into objs), or nullptr
     Order ord;       // item = flattened chunk (nchunk = 1)
     Pass<K, R> p;    // in_off / out_off: row indices (scaled by each object's pitch)
 };
 
-// Workgroup w codes chunk w - chunk0 of the object whose chunk range holds w,
-// found by a binary search over the table's chunk0 (uniform scalar loads that
-// hit the scalar cache after the first workgroups of the launch).
+// Workgroup w codes chunk w - chunk0 of the object whose chunk range holds w:
+// one scalar load from the host's chunk -> object table, or (tables too large
+// to build) a binary search over the entries' chunk0, whose dependent scalar
+// loads a workgroup waits out before its first data load.
 template <int K, int R, int BS, int LAUX, int SAUX>
 __global__ __launch_bounds__(BS) void gf_apply_var(const VarArgs<K, R> a) {
     uint32_t w, unused;
     if (!wg_item(a.ord, w, unused)) return;
     const constant_ptr<VarObj> objs = (constant_ptr<VarObj>)a.objs;
-    uint32_t lo = 0, hi = a.nobj;  // objs[lo].chunk0 <= w < objs[hi].chunk0
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (objs[mid].chunk0 <= w) lo = mid;
-        else hi = mid;
+    uint32_t lo = 0;
+    if (a.chunk_obj) {
+        lo = ((constant_ptr<uint32_t>)a.chunk_obj)[w];
+    } else {
+        uint32_t hi = a.nobj;  // objs[lo].chunk0 <= w < objs[hi].chunk0
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (objs[mid].chunk0 <= w) lo = mid;
+            else hi = mid;
+        }
     }
     const uint64_t base = objs[lo].base;
     const uint32_t nvec = objs[lo].nvec, tail = objs[lo].tail, pitch = objs[lo].pitch;

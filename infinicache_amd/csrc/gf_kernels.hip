@@ -1061,10 +1061,11 @@ hipError_t stage_image(MultiWorkspace &ws, const std::vector<uint8_t> &img, Mult
 namespace {
 
 template <int K, int R>
-hipError_t launch_var_t(const Plan &p, const Sub &s, const VarObj *d_objs, uint32_t nobj, uint32_t total,
-                        uint32_t *d_bad, hipStream_t st) {
+hipError_t launch_var_t(const Plan &p, const Sub &s, const VarObj *d_objs, const uint32_t *d_chunk_obj,
+                        uint32_t nobj, uint32_t total, uint32_t *d_bad, hipStream_t st) {
     VarArgs<K, R> a;
     a.objs = d_objs;
+    a.chunk_obj = d_chunk_obj;
     a.nobj = nobj;
     a.bad = d_bad;
     // row indices, not offsets: pitch 1 (each object's pitch scales them in the kernel)
@@ -1076,8 +1077,8 @@ hipError_t launch_var_t(const Plan &p, const Sub &s, const VarObj *d_objs, uint3
     return hipGetLastError();
 }
 
-typedef hipError_t (*var_fn)(const Plan &, const Sub &, const VarObj *, uint32_t, uint32_t, uint32_t *,
-                             hipStream_t);
+typedef hipError_t (*var_fn)(const Plan &, const Sub &, const VarObj *, const uint32_t *, uint32_t, uint32_t,
+                             uint32_t *, hipStream_t);
 template <int K>
 var_fn pick_var_r(int R) {
     return R == 1 ? &launch_var_t<K, 1> : R == 2 ? &launch_var_t<K, 2> : R == 3 ? &launch_var_t<K, 3>
@@ -1110,9 +1111,19 @@ hipError_t launch_plan_objs(Plan &p, const DevObj *objs, int nobj, uint32_t *d_b
     int maxrow = 0;
     for (int r : p.in_rows) maxrow = std::max(maxrow, r);
     for (int r : p.out_rows) maxrow = std::max(maxrow, r);
-    std::vector<uint8_t> img((size_t)nobj * sizeof(VarObj));
-    VarObj *t = (VarObj *)img.data();
     uint64_t total = 0;
+    for (int o = 0; o < nobj; ++o) total += ((objs[o].shard_len + 15) / 16 + kBlock - 1) / kBlock;
+    if (total >= 0x7ff00000ull) return hipErrorInvalidValue;  // > 2^31 workgroups: split the table
+    // the image: the object table, then (up to 16 Mi chunks, a 64 MiB table)
+    // each chunk's object index, so a workgroup finds its object with one
+    // scalar load instead of a binary search (RSGPU_VAR_SEARCH=1: always search)
+    static const bool force_search = std::getenv("RSGPU_VAR_SEARCH") != nullptr;
+    const bool direct = !force_search && total <= ((uint64_t)1 << 24);
+    const size_t tab_bytes = (size_t)nobj * sizeof(VarObj);
+    std::vector<uint8_t> img(tab_bytes + (direct ? (size_t)total * 4 : 0));
+    VarObj *t = (VarObj *)img.data();
+    uint32_t *cobj = (uint32_t *)(img.data() + tab_bytes);
+    uint64_t c = 0;
     for (int o = 0; o < nobj; ++o) {
         const DevObj &d = objs[o];
         VarObj &v = t[o];
@@ -1122,17 +1133,21 @@ hipError_t launch_plan_objs(Plan &p, const DevObj *objs, int nobj, uint32_t *d_b
         v.pitch = (uint32_t)d.pitch;
         v.span = (uint32_t)((size_t)maxrow * d.pitch + (size_t)v.nvec * 16);
         v.packed = tail_part(d.pitch, v.nvec);
-        v.chunk0 = (uint32_t)total;
-        total += (v.nvec + kBlock - 1) / kBlock;
+        v.chunk0 = (uint32_t)c;
+        const uint32_t nch = (v.nvec + kBlock - 1) / kBlock;
+        if (direct)
+            for (uint32_t j = 0; j < nch; ++j) cobj[c + j] = (uint32_t)o;
+        c += nch;
     }
-    if (total >= 0x7ff00000ull) return hipErrorInvalidValue;  // > 2^31 workgroups: split the table
     std::lock_guard<std::mutex> g(ws.mu);
     MultiWorkspace::Slot *w = nullptr;
     hipError_t e = stage_image(ws, img, w);
     for (int r0 = 0; r0 < p.R && e == hipSuccess; r0 += kMaxR) {
         Sub s{r0, std::min(kMaxR, p.R - r0), 0};
         s.nw = std::max(0, std::min(s.R, p.nw - r0));
-        e = pick_var(p.K, s.R)(p, s, (const VarObj *)w->d, (uint32_t)nobj, (uint32_t)total, d_bad, st);
+        const uint8_t *d = (const uint8_t *)w->d;
+        e = pick_var(p.K, s.R)(p, s, (const VarObj *)d, direct ? (const uint32_t *)(d + tab_bytes) : nullptr,
+                               (uint32_t)nobj, (uint32_t)total, d_bad, st);
     }
     if (e == hipSuccess) e = hipEventRecord(w->done, st);
     return e;
