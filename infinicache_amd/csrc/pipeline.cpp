@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -36,10 +37,19 @@
 namespace {
 
 constexpr int kSlots = 4;
+// slots in the ring (RSGPU_PIPE_SLOTS overrides, measurement only)
+int pipe_slots() {
+    static const int n = [] {
+        const char *e = std::getenv("RSGPU_PIPE_SLOTS");
+        const int v = e ? std::atoi(e) : kSlots;
+        return v >= 1 && v <= 16 ? v : kSlots;
+    }();
+    return n;
+}
 
 int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
     auto &P = ctx->pipe;
-    while ((int)P.slots.size() < kSlots) {
+    while ((int)P.slots.size() < pipe_slots()) {
         std::unique_ptr<PipeSlot> s(new PipeSlot());
         HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         HIP_TRY(hipMalloc(&s->d_bad, 4));
@@ -226,7 +236,7 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
     if ((e = ensure_slots(ctx, maxbytes))) return e;
     hipError_t he = hipSuccess;
     for (int o = 0; o < nobj && he == hipSuccess; ++o) {
-        PipeSlot &s = *ctx->pipe.slots[o % kSlots];
+        PipeSlot &s = *ctx->pipe.slots[o % pipe_slots()];
         const size_t S = shard_lens[o];
         he = hipMemcpyAsync(s.d, objs[o], (size_t)k * S, hipMemcpyHostToDevice, s.stream);
         Layout L{s.d, 0, S, S, 1};
@@ -296,20 +306,31 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
     if ((e = ensure_flags(ctx, nobj))) return e;
     hipError_t he = hipSuccess;
     for (int o = 0; o < nobj && he == hipSuccess; ++o) {
-        PipeSlot &s = *ctx->pipe.slots[o % kSlots];
+        PipeSlot &s = *ctx->pipe.slots[o % pipe_slots()];
         Plan &plan = *plans[o];
         uint8_t *const *row = shards + (size_t)o * n;
         const size_t S = shard_lens[o], P = S;  // packed rows
         const bool checks = plan.nw < plan.R;
-        for (int c = 0; c < plan.K && he == hipSuccess; ++c)
-            he = hipMemcpyAsync(s.d + (size_t)plan.in_rows[c] * P, row[plan.in_rows[c]], S,
-                                hipMemcpyHostToDevice, s.stream);
+        // rows that are neighbours both in the object and in host memory (a
+        // Split image's) go as one copy: per-copy overhead is what a 10-row
+        // Get of a small object spends its time on
+        for (int c = 0; c < plan.K && he == hipSuccess;) {
+            const int r0 = plan.in_rows[c];
+            int m = 1;
+            while (c + m < plan.K && plan.in_rows[c + m] == r0 + m && row[r0 + m] == row[r0] + (size_t)m * S) ++m;
+            he = hipMemcpyAsync(s.d + (size_t)r0 * P, row[r0], (size_t)m * S, hipMemcpyHostToDevice, s.stream);
+            c += m;
+        }
         if (he == hipSuccess && checks) he = hipMemsetAsync(s.d_bad, 0, 4, s.stream);
         if (he == hipSuccess)
             he = launch_plan(plan, slack_layout(s.d, P, S), checks ? s.d_bad : nullptr, s.stream);
-        for (int r = 0; r < plan.nw && he == hipSuccess; ++r)
-            he = hipMemcpyAsync(row[plan.out_rows[r]], s.d + (size_t)plan.out_rows[r] * P, S,
-                                hipMemcpyDeviceToHost, s.stream);
+        for (int r = 0; r < plan.nw && he == hipSuccess;) {
+            const int r0 = plan.out_rows[r];
+            int m = 1;
+            while (r + m < plan.nw && plan.out_rows[r + m] == r0 + m && row[r0 + m] == row[r0] + (size_t)m * S) ++m;
+            he = hipMemcpyAsync(row[r0], s.d + (size_t)r0 * P, (size_t)m * S, hipMemcpyDeviceToHost, s.stream);
+            r += m;
+        }
         if (he == hipSuccess) {
             if (checks)
                 he = hipMemcpyAsync(ctx->pipe.h_bad + o, s.d_bad, 4, hipMemcpyDeviceToHost, s.stream);
