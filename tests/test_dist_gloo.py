@@ -1,4 +1,4 @@
-"""World-size-2 (and 3) CPU rehearsal of bench.py's multi-rank path with the
+"""World-size-2, 3 and 8 CPU rehearsal of bench.py's multi-rank path with the
 gloo backend: object sharding, the all_reduce start/finish barrier and the
 MAX-over-ranks timing.  The per-rank step here codes its
 objects with the CPU oracle so the partition can be checked end to end (a
@@ -55,7 +55,7 @@ def _worker(rank, world, port, nobj_total, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_object_per_rank(world):
     nobj = 11
     ctx = mp.get_context("spawn")
