@@ -386,6 +386,114 @@ __global__ __launch_bounds__(BS) void gf_apply_kernel(
                                                                        chunk * (BS * U) + threadIdx.x, rd);
 }
 
+// Short rows (<= kStagedMaxVec vectors: objects of about 1 KiB), opw objects
+// per workgroup, staged through LDS.  Lane (object, vector) loads straight
+// from HBM (gf_apply_kernel's small form) make every wave load a gather of
+// ~9 row pieces of 112 B; here the workgroup
+//   1. loads its objects' input rows with lanes walking (object, input,
+//      vector) in address order, so each wave load is ~1 KiB of consecutive
+//      rows (as on large objects), into LDS;
+//   2. codes lane (object, vector) from LDS, written rows back into LDS;
+//   3. stores the written rows the same address-ordered way.
+// LDS: opw * (K + R) * nvec * 16 B (<= 64 KiB).  Rows must hold whole
+// vectors (no packed tail) and the batch must not be shard-major.
+constexpr uint32_t kStagedMaxVec = 8;
+__device__ __forceinline__ uint32_t udiv_small(uint32_t x, uint32_t d, float rcp) {
+    uint32_t q = (uint32_t)((float)x * rcp);  // x < 2^16: off by at most one
+    if (q * d > x) --q;
+    else if ((q + 1) * d <= x) ++q;
+    return q;
+}
+
+template <int K, int R, int LAUX, int SAUX>
+__global__ __launch_bounds__(256) void gf_apply_staged(const ApplyArgs<K, R> a) {
+    extern __shared__ u32x4 lds[];  // [opw][K][nvec] inputs, then [opw][R][nvec] written rows
+    uint32_t grp, chunk;
+    if (!wg_item(a.ord, grp, chunk)) return;
+    const uint32_t t = threadIdx.x, nvec = a.nvec, o0 = grp * a.opw;
+    const uint32_t nob = min(a.opw, a.nobj - o0);
+    const uint32_t stride = (uint32_t)a.obj_stride;  // the group spans < 4 GiB (host)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)o0 * a.obj_stride), (short)0, (int)a.gspan, 0x00020000);
+    const float rn = 1.0f / (float)nvec, rkn = 1.0f / (float)(K * nvec);
+    u32x4 *in = lds, *out = lds + a.opw * K * nvec;
+
+    // 1. inputs in address order; every load of a lane issued before its LDS stores
+    const uint32_t nin = nob * K * nvec;
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const uint32_t e = t + i * 256u;
+        if (e < nin) {
+            const uint32_t j = udiv_small(e, K * nvec, rkn), rem = e - j * K * nvec;
+            const uint32_t c = udiv_small(rem, nvec, rn), v = rem - c * nvec;
+            // row offsets of the pass: select with compares (a runtime index
+            // into the kernarg array would go through scratch)
+            uint32_t off = a.p.in_off[0];
+#pragma unroll
+            for (int q = 1; q < K; ++q) off = c == (uint32_t)q ? a.p.in_off[q] : off;
+            x[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, j * stride + off + v * 16u, 0, LAUX);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        if (t + i * 256u < nin) in[t + i * 256u] = x[i];
+    __syncthreads();
+
+    // 2. lane (object j, vector v) codes from LDS
+    const uint32_t j = udiv_small(t, nvec, rn), v = t - j * nvec;
+    if (j < nob) {
+        uint32_t acc[R][4];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const u32x4 y = in[(j * K + c) * nvec + v];
+            if (c >= K - R && c >= K - (int)a.p.ki) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) acc[(R - K + c) < 0 ? 0 : (R - K + c)][d] ^= y[d];
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const GfIdx g = gf_idx(y[d]);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r][d] = gf_mac(acc[r][d], &a.p.tab[(c * R + r) * kTabWords], g);
+                }
+            }
+        }
+        bool mismatch = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if ((uint32_t)r < a.p.nw) {
+                out[(j * R + r) * nvec + v] = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+            } else {
+                const uint32_t valid = (v == nvec - 1) ? a.tail : 16u;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+            }
+        }
+        if (mismatch) a.bad[o0 + j] = 1u;
+        if (a.p.clear && v == 0) a.bad[o0 + j] = 0u;
+    }
+    if (a.p.nw == 0) return;  // uniform: no barrier skipped by part of the group
+    __syncthreads();
+
+    // 3. written rows in address order
+    const uint32_t nwv = a.p.nw * nvec, nout = nob * nwv;
+    const float rnw = 1.0f / (float)nwv;
+    for (uint32_t e = t; e < nout; e += 256u) {
+        const uint32_t jj = udiv_small(e, nwv, rnw), rem = e - jj * nwv;
+        const uint32_t r = udiv_small(rem, nvec, rn), vv = rem - r * nvec;
+        uint32_t off = a.p.out_off[0];
+#pragma unroll
+        for (int q = 1; q < R; ++q) off = r == (uint32_t)q ? a.p.out_off[q] : off;
+        __builtin_amdgcn_raw_buffer_store_b128(out[(jj * R + r) * nvec + vv], rs, jj * stride + off + vv * 16u, 0,
+                                               SAUX);
+    }
+}
+
 // constant address space: uniform invariant data the compiler may (and does)
 // fetch with scalar loads
 template <typename T>

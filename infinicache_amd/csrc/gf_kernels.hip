@@ -401,6 +401,18 @@ inline unsigned pass_lds(int K, int nw, int R) {
     return store_lds(K);
 }
 
+// The LDS-staged small-object form (gf_apply_staged) for rows of at most
+// kStagedMaxVec whole vectors of an object-major batch; RSGPU_STAGED=0 turns
+// it off (measurement)
+template <int K, int R>
+inline bool use_staged(uint32_t nvec, const Pass<K, R> &p) {
+    static const bool on = [] {
+        const char *e = std::getenv("RSGPU_STAGED");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on && nvec <= kStagedMaxVec && p.packed == 0 && p.sub_stride == 0;
+}
+
 template <int K, int R>
 hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
                         hipStream_t st);
@@ -447,12 +459,18 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
                 a.nobj = (uint32_t)std::min<size_t>((size_t)ng * opw, (size_t)L.nobj - o0);
                 unsigned grid;
                 a.ord = make_order(1, (uint32_t)ng, (size_t)a.nobj * L.obj_stride, grid);
-                // (staging the group through LDS so that every wave load is
-                // ~1 KiB of consecutive rows measured +6 points at 1 KiB
-                // encode, 0 on decode and -7 / -4 points at 4 / 16 KiB:
-                // tools/kbench KB_SET=small, not shipped)
-                hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormSmall>),
-                                   dim3(grid), dim3(kBlock), pass_lds(K, (int)a.p.nw, R), st, a);
+                // rows of <= 8 vectors (objects of ~1 KiB) staged through LDS
+                // so that every wave load is ~1 KiB of consecutive rows
+                // (gf_apply_staged); longer rows lose with it (kbench KB_SET=
+                // small: -7 / -4 points at 4 / 16 KiB)
+                if (use_staged(a.nvec, a.p)) {
+                    const unsigned lds = opw * (unsigned)(K + R) * a.nvec * 16u;
+                    hipLaunchKernelGGL((gf_apply_staged<K, R, kLoadAux, kStoreAux>), dim3(grid), dim3(kBlock),
+                                       std::max(lds, pass_lds(K, (int)a.p.nw, R)), st, a);
+                } else {
+                    hipLaunchKernelGGL((gf_apply_kernel<K, R, kUnroll, kBlock, kLoadAux, kStoreAux, kFormSmall>),
+                                       dim3(grid), dim3(kBlock), pass_lds(K, (int)a.p.nw, R), st, a);
+                }
                 hipError_t e = hipGetLastError();
                 if (e != hipSuccess) return e;
             }
