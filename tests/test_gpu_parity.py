@@ -478,10 +478,15 @@ def test_dev_many_objects_grid_y_split(gpu):
                                                    (3, 1, 1000, 100, 4096, 16),
                                                    (10, 2, 103, 1001, 0, 4), (10, 2, 103, 999, 0, 1),
                                                    (10, 4, 1, 700, 0, 1), (10, 2, 17, 513, 3, 1),
-                                                   (10, 2, 4097, 20, 0, 1), (6, 3, 29, 300, 5, 4)])
+                                                   (10, 2, 4097, 20, 0, 1), (6, 3, 29, 300, 5, 4),
+                                                   # rows of <= 8 whole vectors: the LDS-staged form
+                                                   # (K + R up to 20: 80 KiB of LDS per workgroup)
+                                                   (12, 4, 128, 500, 0, 16), (16, 4, 100, 300, 32, 16),
+                                                   (2, 1, 5, 1000, 0, 16), (15, 1, 64, 777, 16, 16)])
 def test_dev_small_objects_packed_workgroups(gpu, k, p, S, nobj, gap, palign):
     """Rows of <= 128 vectors: a workgroup codes 256 // nvec whole objects
-    (gf_kernels.hip launch_fixed, opw > 1).  Encode the whole batch against
+    (gf_kernels.hip launch_fixed, opw > 1; rows of <= 8 whole vectors go
+    through LDS, gf_apply_staged).  Encode the whole batch against
     the oracle, per-object Verify flags, fused decode and data-only
     reconstruct; ragged last group, strides with gaps between objects.
     palign < 16: pitches below 16 * ceil(S / 16) down to byte-packed rows
