@@ -420,113 +420,9 @@ std::vector<Variant> rows_variants() {
     };
 }
 
-// Experiment (KB_SET=small, not shipped): small objects staged through LDS
-// (rows of <= 128 vectors, ApplyArgs::opw objects per workgroup, row pitch
-// % 16 == 0).  Coding lane by lane from
-// HBM (gf_apply_kernel's opw > 1 form) makes every wave load a gather of
-// ~9 short row pieces, one per object; here the workgroup instead
-//   1. loads its objects' input rows with lanes walking (object, input,
-//      vector) in address order: each wave load is ~1 KiB of consecutive
-//      rows, as on large objects;
-//   2. codes lane (object, vector) from LDS, outputs back into LDS;
-//   3. stores the output rows the same address-ordered way.
-// LDS: opw * (K + R) * nvec * 16 B (<= 64 KiB for K + R <= 16).
-__device__ __forceinline__ uint32_t div_small(uint32_t x, uint32_t d, float rcp) {
-    uint32_t q = (uint32_t)((float)x * rcp);  // x < 2^16 here: off by at most one
-    if (q * d > x) --q;
-    else if ((q + 1) * d <= x) ++q;
-    return q;
-}
-
-template <int K, int R, int LAUX, int SAUX>
-__global__ __launch_bounds__(256) void gf_apply_small(const ApplyArgs<K, R> a) {
-    extern __shared__ u32x4 lds[];  // [opw][K][nvec] inputs, then [opw][R][nvec] outputs
-    __shared__ uint32_t off_in[K], off_out[R];
-    uint32_t grp, chunk;
-    if (!wg_item(a.ord, grp, chunk)) return;
-    const uint32_t t = threadIdx.x, nvec = a.nvec, o0 = grp * a.opw;
-    const uint32_t nob = min(a.opw, a.nobj - o0);
-    const uint32_t stride = (uint32_t)a.obj_stride;  // (opw-1)*stride < 4 GiB (host)
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-        if (t == (uint32_t)c) off_in[c] = a.p.in_off[c];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (t == (uint32_t)(K + r)) off_out[r] = a.p.out_off[r];
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(a.base + (uint64_t)o0 * a.obj_stride), (short)0, (int)a.gspan, 0x00020000);
-    const float rn = 1.0f / (float)nvec, rkn = 1.0f / (float)(K * nvec);
-    u32x4 *in = lds, *out = lds + a.opw * K * nvec;
-
-    // 1. inputs, address order; all loads of a lane issued before its LDS stores
-    const uint32_t nin = nob * K * nvec;
-    u32x4 x[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        const uint32_t e = t + i * 256u;
-        if (e < nin) {
-            const uint32_t j = div_small(e, K * nvec, rkn), rem = e - j * K * nvec;
-            const uint32_t c = div_small(rem, nvec, rn), v = rem - c * nvec;
-            x[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, j * stride + off_in[c] + v * 16u, 0, LAUX);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-        if (t + i * 256u < nin) in[t + i * 256u] = x[i];
-    __syncthreads();
-
-    // 2. code lane (object j, vector v) from LDS
-    const uint32_t j = div_small(t, nvec, rn), v = t - j * nvec;
-    if (j < nob) {
-        uint32_t acc[R][4];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) acc[r][d] = 0;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const u32x4 y = in[(j * K + c) * nvec + v];
-            if (c >= K - R && c >= K - (int)a.p.ki) {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) acc[(R - K + c) < 0 ? 0 : (R - K + c)][d] ^= y[d];
-            } else {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const GfIdx g = gf_idx(y[d]);
-#pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        acc[r][d] = gf_mac(acc[r][d], &a.p.tab[(c * R + r) * kTabWords], g);
-                }
-            }
-        }
-        bool mismatch = false;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if ((uint32_t)r < a.p.nw) {
-                out[(j * R + r) * nvec + v] = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-            } else {
-                const uint32_t valid = (v == nvec - 1) ? a.tail : 16u;
-#pragma unroll
-                for (int d = 0; d < 4; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
-            }
-        }
-        if (mismatch) a.bad[o0 + j] = 1u;
-        if (a.p.clear && v == 0) a.bad[o0 + j] = 0u;
-    }
-    if (a.p.nw == 0) return;  // uniform: no barrier skipped by part of the group
-    __syncthreads();
-
-    // 3. outputs, address order
-    const uint32_t nout = nob * a.p.nw * nvec, nwv = a.p.nw * nvec;
-    const float rnw = 1.0f / (float)nwv;
-    for (uint32_t e = t; e < nout; e += 256u) {
-        const uint32_t jj = div_small(e, nwv, rnw), rem = e - jj * nwv;
-        const uint32_t r = div_small(rem, nvec, rn), vv = rem - r * nvec;
-        __builtin_amdgcn_raw_buffer_store_b128(out[(jj * R + r) * nvec + vv], rs,
-                                               jj * stride + off_out[r] + vv * 16u, 0, SAUX);
-    }
-}
+// KB_SET=small: the LDS-staged small-object kernel is the library's
+// gf_apply_staged (gf_device.h; shipped for rows of <= 8 vectors since round
+// 3), timed here at every row length against the register form.
 
 // KB_SET=small: the packed small-object launch (opw objects per workgroup,
 // gf_kernels.hip launch_fixed) under other load/store policies and caps.
@@ -544,7 +440,7 @@ void launch_small(const void *args, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, LAUX, SAUX>), dim3(nb), dim3(256),
                        W < 0 ? 0u : 160u * 1024u / (unsigned)w - 256u, st, a);
 }
-// the LDS-staged small-object kernel (gf_apply_small); W > 0: at most W
+// the LDS-staged small-object kernel (gf_apply_staged); W > 0: at most W
 // workgroups per CU through a larger LDS reservation
 template <int K, int R, int LAUX, int SAUX, int W>
 void launch_small_lds(const void *args, dim3 grid, hipStream_t st) {
@@ -557,7 +453,7 @@ void launch_small_lds(const void *args, dim3 grid, hipStream_t st) {
     a.ord = order_for<0>(dim3(1, (nobj + opw - 1) / opw), 0, nb);
     unsigned lds = opw * (K + R) * a.nvec * 16u;
     if (W > 0) lds = std::max(lds, 160u * 1024u / (unsigned)W - 256u);
-    hipLaunchKernelGGL((gf_apply_small<K, R, LAUX, SAUX>), dim3(nb), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((gf_apply_staged<K, R, LAUX, SAUX>), dim3(nb), dim3(256), lds, st, a);
 }
 template <int K, int R>
 std::vector<Variant> small_variants() {
