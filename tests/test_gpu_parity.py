@@ -592,6 +592,35 @@ def test_decode_batch_mixed_patterns(gpu):
                 assert np.array_equal(objs[i][j], fulls[i][j]), (i, j)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_decode_batch_split_images(gpu, pinned):
+    """Gets whose shard buffers are one Split image (rows neighbours in host
+    memory): the pipeline merges the copies of neighbouring rows (survivors
+    {1-4}, {6-11}; lost {2, 3} written back as one copy).  One object has a
+    row moved to a buffer of its own, which splits its runs."""
+    k, p = 10, 4
+    n = k + p
+    enc = ia.New(k, p)
+    cases = [((0, 5), 104858), ((2, 3), 999), ((10, 11), 4097), ((0, 1, 2, 3), 65536), ((13,), 17),
+             ((4,), 1), ((0, 5), 3001)]
+    objs, pres, fulls = [], [], []
+    for i, (lost, S) in enumerate(cases):
+        full = _full(k, p, S, idx=700 + i)
+        buf = ia.host_alloc(n * S) if pinned else np.empty(n * S, np.uint8)
+        rows = [buf[j * S:(j + 1) * S] for j in range(n)]
+        for j in range(n):
+            rows[j][:] = 0xA5 if j in lost else full[j]
+        if i == len(cases) - 1:
+            rows[7] = full[7].copy()  # not next to rows 6 and 8 any more
+        objs.append(rows)
+        pres.append([j not in lost for j in range(n)])
+        fulls.append(full)
+    assert enc.decode_batch(objs, present=pres) == [True] * len(cases)
+    for i in range(len(cases)):
+        for j in range(n):
+            assert np.array_equal(objs[i][j], fulls[i][j]), (i, j)
+
+
 # ------------------------------------------------ mixed erasure patterns
 
 @pytest.mark.parametrize("k,p,S,nobj", [(10, 2, 50001, 300), (10, 4, 7777, 120), (20, 4, 3000, 40),
