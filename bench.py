@@ -317,20 +317,25 @@ def timed_run(step, steps, warmup, sync, dctx: DistCtx):
 def pmc_traffic(kernel_key, workload, alg_bytes):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (separate
     --pmc passes; gfx950 FETCH_SIZE x2 correction, MI355X_MICROARCH.md §HBM),
-    only when that summary was taken on this same workload and launch size."""
+    only when that summary was taken on this same workload and launch size.
+    Returns (bytes or None, where they came from): the counters are NOT
+    collected inside this run (a --pmc pass is its own rocprofv3 process)."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
     if not os.path.exists(path):
         path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    rel = os.path.relpath(path, ROOT)
     try:
         d = json.load(open(path))
         if d.get("workload", "encdec") != workload:
-            return None
+            return None, f"none: {rel} is for another workload"
         k = d["kernels"][kernel_key]
         if k.get("algorithmic_bytes_per_launch") != alg_bytes:
-            return None
-        return k["hbm_bytes_per_launch"]
+            return None, f"none: {rel} is for another launch size"
+        src = (f"committed profile {rel} (rocprofv3 --pmc passes of this workload and launch size, "
+               f"{d.get('source', 'see the file')}); not measured in this run")
+        return k["hbm_bytes_per_launch"], src
     except Exception:
-        return None
+        return None, f"none: no committed PMC summary for {kernel_key}"
 
 
 def run_trace(args):
@@ -848,7 +853,7 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     # every rank's own kernel rate (N > 1: each GPU codes its own objects)
     frac_ranks = [round(a / HBM_PEAK_GBS, 4) for a in dctx.gather(achieved)]
-    traffic = pmc_traffic(kernel_key, args.workload, dom_bytes)
+    traffic, traffic_src = pmc_traffic(kernel_key, args.workload, dom_bytes)
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -856,6 +861,7 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
+        "traffic_source": traffic_src,
         "kernel": f"{kernel_key} ({dom} launches), {dom_bytes} algorithmic B/launch, "
                   f"{dom_ms * 1e3:.1f} us avg (HIP events around {args.steps} back-to-back launches "
                   f"per op after the timed steps, scaled x{scale:.4f} to the timed step)",
@@ -880,8 +886,11 @@ def main():
                     "Cache, so this is not an HBM rate (reported for comparison, not the value)",
         }
 
+    # The CPU baseline at every world size (north_star: "next to the Go CPU
+    # path ... in the same run"): rank 0 times the CPU port after the timed
+    # region and its barriers, on its own batch 0 (bit-compared with its GPU).
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and not w.get("shard_major"):
+    if rank == 0 and not args.no_cpu and not w.get("shard_major"):
         from oracle import rs_numpy as rn
         ns = min(256, nobj)  # 256 x 1.26 MB: well beyond the host's last-level cache
         # final GPU state of the sampled objects: batch 0 after check_ops, so

@@ -275,6 +275,30 @@ int rsgpu_reconstruct_dev_masks(rsgpu_ctx *ctx, void *d_base, const uint32_t *d_
                                 size_t pitch, size_t obj_stride, int nobj, int data_only,
                                 uint32_t *d_status, void *stream);
 
+/* ---- shard-major Get batches on whole lines ------------------------------
+ * A Get batch of small objects decodes fastest shard-major through the
+ * *_dev_masks calls with every piece on whole 128-B lines: at a 112-B stride
+ * (1 KiB objects, shard_len 103) each rebuilt piece straddles two lines and
+ * the decode runs at 41 % of HBM peak, at a 128-B stride it rewrites whole
+ * lines.  (Replaces hand-laid batches behind
+ * proxy/lambdastore/connection.go:274-306: every Get batch is mixed-pattern.)
+ * rsgpu_shardmajor_layout returns that geometry for nobj pieces of shard_len
+ * bytes: obj_stride = shard_len rounded up to 128 when the gap is at most
+ * shard_len/4 (the encode still codes the batch as one object), else to 16;
+ * pitch = nobj*obj_stride rounded up to 256. */
+int rsgpu_shardmajor_layout(size_t shard_len, int nobj, size_t *obj_stride, size_t *pitch);
+/* Device copy of the pieces of rows `rows` (bit i: row i; i < data+parity):
+ * for every object o < nobj and such row i, shard_len bytes from
+ * d_src + i*src_pitch + o*src_obj_stride to d_dst + i*dst_pitch +
+ * o*dst_obj_stride, exactly (nothing else is written).  Either side may be
+ * object-major or shard-major (the *_dev layouts above), at any alignment;
+ * source and destination must not overlap.  Moves a batch into the
+ * rsgpu_shardmajor_layout geometry before a *_dev_masks call (the rows that
+ * arrived) and the rebuilt rows back after it.  Asynchronous on `stream`. */
+int rsgpu_copy_pieces(rsgpu_ctx *ctx, const void *d_src, size_t src_pitch, size_t src_obj_stride, void *d_dst,
+                      size_t dst_pitch, size_t dst_obj_stride, size_t shard_len, int nobj, uint64_t rows,
+                      void *stream);
+
 /* ---- variable-size device-resident batches ------------------------------
  * Objects of ANY sizes in one launch per pass (config 5's objects range from
  * 4 KiB to 100 MiB, client/ecRedis.go:96): objs[o] (a host array) describes

@@ -26,7 +26,8 @@ EXPORTS = (
     "rsgpu_create_multi", "rsgpu_devices", "rsgpu_encode_image", "rsgpu_encode_verify_image",
     "rsgpu_verify_image", "rsgpu_reconstruct_image", "rsgpu_decode_image", "rsgpu_device_calls",
     "rsgpu_encode_dev_objs", "rsgpu_verify_dev_objs", "rsgpu_reconstruct_dev_objs", "rsgpu_decode_dev_objs",
-    "rsgpu_worker_start", "rsgpu_worker_stop", "rsgpu_worker_stats",
+    "rsgpu_worker_start", "rsgpu_worker_stop", "rsgpu_worker_stats", "rsgpu_shardmajor_layout",
+    "rsgpu_copy_pieces",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -109,6 +110,8 @@ def load():
     L.rsgpu_worker_stop.argtypes = [vp]
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.rsgpu_worker_stats.argtypes = [vp, u64p, u64p, u64p]
+    L.rsgpu_shardmajor_layout.argtypes = [sz, ci, szp, szp]
+    L.rsgpu_copy_pieces.argtypes = [vp, vp, sz, sz, vp, sz, sz, sz, ci, ctypes.c_uint64, vp]
     L.rsgpu_encode_batch.argtypes = [vp, u8pp, szp, ci]
     L.rsgpu_decode_batch.argtypes = [vp, u8pp, u8p, szp, ci, intp]
     L.rsgpu_host_register.argtypes = [vp, sz]

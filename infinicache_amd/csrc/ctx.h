@@ -3,10 +3,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -32,10 +34,10 @@ struct Slot {
     uint32_t *m_bad = nullptr;  // device address of h_bad (mapped pinned memory)
     ~Slot() {
         if (stream) (void)hipStreamDestroy(stream);
-        if (h) (void)hipHostFree(h);
-        if (d) (void)hipFree(d);
-        if (d_bad) (void)hipFree(d_bad);
-        if (h_bad) (void)hipHostFree(h_bad);
+        retire(h, true);
+        retire(d, false);
+        retire(d_bad, false);
+        retire(h_bad, true);
     }
 };
 
@@ -78,8 +80,8 @@ struct PipeSlot {
     uint32_t *d_bad = nullptr;
     ~PipeSlot() {
         if (stream) (void)hipStreamDestroy(stream);
-        if (d) (void)hipFree(d);
-        if (d_bad) (void)hipFree(d_bad);
+        retire(d, false);
+        retire(d_bad, false);
     }
 };
 
@@ -88,9 +90,7 @@ struct Pipeline {
     std::vector<std::unique_ptr<PipeSlot>> slots;
     uint32_t *h_bad = nullptr;  // pinned, one flag per object of the batch
     size_t h_bad_cap = 0;
-    ~Pipeline() {
-        if (h_bad) (void)hipHostFree(h_bad);
-    }
+    ~Pipeline() { retire(h_bad, true); }
 };
 
 // Device atlas of every erasure pattern of one operation (gf_masked.h),
@@ -112,9 +112,9 @@ struct Atlas {
     std::vector<uint32_t> h_tabs; // kernel tables (freed after the upload unless shared)
     AtlasView view;
     void free_dev() {
-        if (d_pat) (void)hipFree(d_pat);
-        if (d_recs) (void)hipFree(d_recs);
-        if (d_tabs) (void)hipFree(d_tabs);
+        retire(d_pat, false);
+        retire(d_recs, false);
+        retire(d_tabs, false);
         d_pat = nullptr;
         d_recs = nullptr;
         d_tabs = nullptr;
@@ -129,9 +129,6 @@ enum AtlasMode { kAtlasReconstruct = 0, kAtlasData = 1, kAtlasDecode = 2 };
 
 // The resident per-object coder (gf_worker.hip, rsgpu_worker_start).
 struct Worker;
-struct WorkerDeleter {
-    void operator()(Worker *w) const;
-};
 constexpr int kWorkerDeclined = 1;  // worker_run: not served here, take the stream path
 
 }  // namespace rsgpu
@@ -145,7 +142,9 @@ struct rsgpu_ctx {
     uint32_t *d_ctab = nullptr;      // [256][8] coefficient tables (gf_apply_lanes)
     std::mutex ctab_mu;              // guards the d_ctab upload (retried after a failure)
     rsgpu::StatusScratch scratch;    // multi-reporter status of the masked decode
-    std::unique_ptr<rsgpu::Worker, rsgpu::WorkerDeleter> worker;  // rsgpu_worker_start (nullptr: off)
+    // rsgpu_worker_start (null: off); read with std::atomic_load: a call in
+    // flight keeps the worker alive while a stop detaches it
+    std::shared_ptr<rsgpu::Worker> worker;
     std::mutex worker_mu;            // starts and stops
     // Multi-device context (rsgpu_create_multi / RSGPU_ALL_DEVICES): one
     // single-device context per entry of the device list.  Per-object calls
@@ -160,9 +159,7 @@ struct rsgpu_ctx {
     bool multi() const { return !subs.empty(); }
     rsgpu_ctx *pick() { return subs[rr.fetch_add(1, std::memory_order_relaxed) % subs.size()].get(); }
     rsgpu_ctx *sub_for(const void *dev_ptr);  // rsgpu.cpp; nullptr: not memory of one of our devices
-    ~rsgpu_ctx() {
-        if (d_ctab) (void)hipFree(d_ctab);
-    }
+    ~rsgpu_ctx() { retire(d_ctab, false); }
     int k = 0, p = 0, n = 0;
     unsigned kind = 0;
     int device = 0;
@@ -181,13 +178,14 @@ struct rsgpu_ctx {
     // its own duration and gives the calling thread its previous device back
     // on return (the guard), so a process driving several GPUs from one thread
     // never finds its current device switched under it.
-    int use_device(DeviceGuard &g) {
+    // compute = false: worker start / stop (not counted in `calls`)
+    int use_device(DeviceGuard &g, bool compute = true) {
         {
             std::lock_guard<std::mutex> l(mu);
             if (dev_state == 0) dev_state = rsgpu_device_ok(device) ? 1 : RSGPU_ERR_NO_DEVICE;
             if (dev_state < 0) return dev_state;
         }
-        calls.fetch_add(1, std::memory_order_relaxed);
+        if (compute) calls.fetch_add(1, std::memory_order_relaxed);
         int cur = -1;
         HIP_TRY(hipGetDevice(&cur));
         if (cur != device) {
@@ -381,10 +379,12 @@ struct rsgpu_ctx {
             HIP_TRY(hipHostGetDevicePointer((void **)&s->m_bad, s->h_bad, 0));
         }
         if (s->cap < bytes) {
-            if (s->h) (void)hipHostFree(s->h);
-            if (s->d) (void)hipFree(s->d);
+            // the old images are retired (freed at once unless a worker runs);
+            // growth at least 1.5x bounds what a running worker keeps
+            retire(s->h, true);
+            retire(s->d, false);
+            const size_t cap = round_up(std::max(bytes, s->cap + s->cap / 2), (size_t)1 << 20);
             s->h = nullptr; s->d = nullptr; s->hdev = nullptr; s->cap = 0;
-            const size_t cap = round_up(bytes, (size_t)1 << 20);
             HIP_TRY(hipHostMalloc(&s->h, cap, hipHostMallocDefault));
             HIP_TRY(hipHostGetDevicePointer((void **)&s->hdev, s->h, 0));
             HIP_TRY(hipMalloc(&s->d, cap));
@@ -414,5 +414,10 @@ void *host_device_ptr(const void *p, size_t len);
 // with *bad = 0 / 1 (a check failed), kWorkerDeclined (no worker, too large,
 // every mailbox busy: the caller takes the stream path) or an error.
 int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *const *rows, uint32_t *bad);
-int worker_stop(rsgpu_ctx *ctx);
+// Runs fn with every worker of the process parked: calls in flight finish,
+// each resident kernel leaves, later calls take the stream path until fn
+// returns (the next one relaunches).  For runtime calls that synchronise the
+// device on behalf of the user (rsgpu_host_free / _unregister): they then
+// return at once instead of waiting for the workers to idle out.
+int with_workers_parked(const std::function<int()> &fn);
 }  // namespace rsgpu

@@ -20,6 +20,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "devmem.h"
+
 namespace rsgpu {
 
 // Kernel coefficient format: a coefficient c is stored as five u32 words of

@@ -78,9 +78,9 @@ int Plan::identity_inputs() const {
 }
 
 Plan::~Plan() {
-    if (d_tab) (void)hipFree(d_tab);
-    if (d_in_row) (void)hipFree(d_in_row);
-    if (d_tab3) (void)hipFree(d_tab3);
+    retire(d_tab, false);
+    retire(d_in_row, false);
+    retire(d_tab3, false);
 }
 
 // Generic pass for K > 16 inputs (any shard count up to 256) and up to
@@ -742,13 +742,13 @@ static hipError_t upload_generic(Plan &p) {
         }
     hipError_t e = hipMalloc(&p.d_tab, t.size() * 4);
     if (e == hipSuccess) e = hipMalloc(&p.d_tab3, t3.size() * 4);
-    if (e == hipSuccess) e = hipMemcpy(p.d_tab3, t3.data(), t3.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload(p.d_tab3, t3.data(), t3.size() * 4);
     if (e == hipSuccess) e = hipMalloc(&p.d_in_row, rows.size() * 4);
-    if (e == hipSuccess) e = hipMemcpy(p.d_tab, t.data(), t.size() * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p.d_in_row, rows.data(), rows.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload(p.d_tab, t.data(), t.size() * 4);
+    if (e == hipSuccess) e = upload(p.d_in_row, rows.data(), rows.size() * 4);
     if (e != hipSuccess) {
         for (uint32_t **d : {&p.d_tab, &p.d_tab3, &p.d_in_row}) {
-            if (*d) (void)hipFree(*d);
+            retire(*d, false);
             *d = nullptr;
         }
         return e;
@@ -965,8 +965,8 @@ MultiWorkspace::~MultiWorkspace() {
     if (upload) (void)hipStreamDestroy(upload);
     for (auto &s : slot) {
         if (s.done) (void)hipEventDestroy(s.done);
-        if (s.d) (void)hipFree(s.d);
-        if (s.h) (void)hipHostFree(s.h);
+        retire(s.d, false);
+        retire(s.h, true);
     }
 }
 
@@ -1055,8 +1055,8 @@ hipError_t stage_image(MultiWorkspace &ws, const std::vector<uint8_t> &img, Mult
         if (e != hipSuccess) return e;
     }
     if (w.cap < img.size()) {
-        if (w.d) (void)hipFree(w.d);
-        if (w.h) (void)hipHostFree(w.h);
+        retire(w.d, false);  // (freed once no worker runs: devmem.cpp)
+        retire(w.h, true);
         w.d = nullptr;
         w.h = nullptr;
         w.cap = 0;

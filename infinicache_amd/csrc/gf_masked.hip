@@ -131,10 +131,10 @@ hipError_t StatusScratch::acquire(size_t nobj, hipStream_t stream, Slot *&s) {
     if (s->done) e = hipEventSynchronize(s->done);  // the call that used it kRing calls ago
     else e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
     if (e == hipSuccess && s->cap < nobj) {
-        if (s->d) (void)hipFree(s->d);
+        const size_t cap = std::max<size_t>({nobj, 1024, s->cap * 2});
+        retire(s->d, false);  // (freed once no worker runs: devmem.cpp)
         s->d = nullptr;
         s->cap = 0;
-        const size_t cap = std::max<size_t>(nobj, 1024);
         e = hipMalloc(&s->d, cap * 2 * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMemsetAsync(s->d, 0, cap * 2 * sizeof(uint32_t), stream);
         if (e == hipSuccess) s->cap = cap;
@@ -148,7 +148,7 @@ hipError_t StatusScratch::release(Slot *s, hipStream_t stream, bool ok) {
     if (!ok || e != hipSuccess) {
         // a failed launch may leave counters set: re-zero on the next use
         (void)hipStreamSynchronize(stream);
-        if (s->d) (void)hipFree(s->d);
+        retire(s->d, false);
         s->d = nullptr;
         s->cap = 0;
     }
@@ -159,7 +159,7 @@ hipError_t StatusScratch::release(Slot *s, hipStream_t stream, bool ok) {
 StatusScratch::~StatusScratch() {
     for (auto &s : slot) {
         if (s.done) (void)hipEventDestroy(s.done);
-        if (s.d) (void)hipFree(s.d);
+        retire(s.d, false);
     }
 }
 

@@ -38,9 +38,10 @@ struct alignas(64) WorkerReq {
     uint64_t g[8];  // low 32 bits: payload (WorkerField), high 32 bits: tag (request number)
 };
 struct alignas(64) WorkerResp {
-    uint64_t done;    // low: last request number served, high: its status (0 ok, 1 mismatch)
-    uint32_t exited;  // the launch generation whose workgroup left this slot
-    uint32_t pad[13];
+    uint64_t done;     // low: last request number served, high: its status (0 ok, 1 mismatch)
+    uint32_t exited;   // the launch generation whose workgroup left this slot
+    uint32_t started;  // the launch generation whose workgroup polls this slot (written before its first poll)
+    uint32_t pad[12];  // [0..4]: trace stamps (RSGPU_WORKER_TRACE)
 };
 struct alignas(64) WorkerSlot {
     WorkerReq req;

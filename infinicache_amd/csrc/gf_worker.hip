@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <set>
 #include <thread>
 
@@ -97,6 +98,12 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
         lt[t][1] = ct[1];
     }
     WorkerSlot *ms = a.slots + blockIdx.x;
+    // the start mark reaches host memory before this workgroup's first poll
+    // of the request line: a caller that sees no mark after taking its
+    // request back knows no poll of this launch can have read it
+    // (post_and_wait's deadline)
+    if (t == 0) __hip_atomic_store(&ms->resp.started, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");  // store -> later loads (system scope; once per launch)
     // the last request served on this slot (by this or an earlier launch)
     uint32_t last = rfl((uint32_t)__hip_atomic_load(&ms->resp.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
@@ -408,7 +415,9 @@ struct Worker {
     size_t stage_cap = 0;
     std::vector<uint32_t> seq;                          // per slot: last request number posted
     std::atomic<uint64_t> free_mask{0};                 // bit i: slot i free
-    hipStream_t stream = nullptr;                       // its own hardware queue (CU-mask stream)
+    std::atomic<bool> closed{false};                    // stopped: every later call is declined
+    std::atomic<int> parked{0};                         // parked (with_workers_parked): calls are declined
+    hipStream_t stream = nullptr;                       // its own hardware queue (worker_stream)
     uint64_t *d_state = nullptr;                        // [0] activity (realtime), [1] closing
     void *d_enc = nullptr, *d_ver = nullptr;            // Encode / Verify records
     uint32_t *d_enc_tab = nullptr, *d_ver_tab = nullptr;  // their v_perm tables [nsub][K][R][5]
@@ -416,27 +425,27 @@ struct Worker {
     int rm = 4;                                         // kernel instantiation: min(4, parity)
     AtlasView views[3];
     uint64_t idle_ticks = 0;
+    std::chrono::nanoseconds timeout{0};                // post_and_wait's deadline for an unstarted workgroup
     std::mutex mu;                                      // launches
     std::atomic<uint32_t> gen{1};                       // the launch the mailboxes belong to
-    std::atomic<uint64_t> served{0}, declined{0}, launches{0};  // rsgpu_worker_stats
+    std::atomic<uint64_t> served{0}, declined{0}, launches{0}, retracted{0};  // rsgpu_worker_stats
     int k = 0;
     bool trace = false;                                 // RSGPU_WORKER_TRACE: device stamps per request
     // trace sums per op: [op][0] requests, [1..5] device stamps (10 ns), [6] host post->response (ns)
     std::atomic<uint64_t> tr[6][7] = {};
     ~Worker() {
+        // (the kernel has left: rsgpu_worker_stop; these free at once
+        // unless another worker still runs, devmem.cpp)
         if (stream) (void)hipStreamDestroy(stream);
-        if (h_slots) (void)hipHostFree(h_slots);
-        for (uint8_t *p : stage_h)
-            if (p) (void)hipHostFree(p);
-        if (d_state) (void)hipFree(d_state);
-        if (d_enc) (void)hipFree(d_enc);
-        if (d_ver) (void)hipFree(d_ver);
-        if (d_enc_tab) (void)hipFree(d_enc_tab);
-        if (d_ver_tab) (void)hipFree(d_ver_tab);
+        retire(h_slots, true);
+        for (uint8_t *p : stage_h) retire(p, true);
+        retire(d_state, false);
+        retire(d_enc, false);
+        retire(d_ver, false);
+        retire(d_enc_tab, false);
+        retire(d_ver_tab, false);
     }
 };
-
-void WorkerDeleter::operator()(Worker *w) const { delete w; }
 
 namespace {
 
@@ -477,10 +486,43 @@ std::vector<uint32_t> record_tables(const std::vector<PatRec> &recs, int K, int 
     return t;
 }
 
-hipError_t upload(const std::vector<PatRec> &r, void *&d) {
+hipError_t upload_records(const std::vector<PatRec> &r, void *&d) {
     hipError_t e = hipMalloc(&d, r.size() * sizeof(PatRec));
-    if (e == hipSuccess) e = hipMemcpy(d, r.data(), r.size() * sizeof(PatRec), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload(d, r.data(), r.size() * sizeof(PatRec));
     return e;
+}
+
+// The resident kernel's stream.  It must be a hardware queue of its own (a
+// stream sharing the worker's queue runs nothing while the kernel is
+// resident) and non-blocking (a blocking stream makes every null-stream call
+// of the process — a synchronous hipMemcpy, PyTorch's default stream — wait
+// for the kernel to idle out).  Measured with a resident kernel on each kind
+// (tools/sync_probe.hip, profiles/r04_sync_probe.txt):
+//   * hipExtStreamCreateWithCUMask (round 3): own queue, but blocking —
+//     null-stream hipMemcpy and hipMallocAsync/hipFreeAsync on another
+//     stream waited for it;
+//   * a plain non-blocking stream: shares the 4 normal-priority queues —
+//     kernels on other streams waited for it;
+//   * non-blocking at the greatest priority: kernels on 8 other streams, the
+//     null stream and stream-ordered allocation ran at once.
+// So the worker takes the last (RSGPU_WORKER_STREAM=cumask keeps round 3's).
+// The device-wide calls (hipFree, hipHostFree, hipHostUnregister) wait on
+// every kind: devmem.cpp and with_workers_parked keep them off the paths
+// that run beside the worker.
+hipError_t worker_stream(int device, hipStream_t &out) {
+    const char *kind = std::getenv("RSGPU_WORKER_STREAM");
+    if (kind && std::strcmp(kind, "cumask") == 0) {
+        int cus = 0;
+        hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (e != hipSuccess) return e;
+        std::vector<uint32_t> cu_mask((size_t)(cus + 31) / 32, 0xffffffffu);
+        if (cus % 32) cu_mask.back() = (1u << (cus % 32)) - 1;
+        return hipExtStreamCreateWithCUMask(&out, (uint32_t)cu_mask.size(), cu_mask.data());
+    }
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(&out, hipStreamNonBlocking, greatest);
 }
 
 // launch generation `g` of the worker (w->mu held)
@@ -529,6 +571,14 @@ int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard
     w->k = ctx->k;
     w->trace = std::getenv("RSGPU_WORKER_TRACE") != nullptr;
     w->idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
+    {
+        // RSGPU_WORKER_TIMEOUT_US: how long a posted request may wait for its
+        // slot's workgroup to start polling before it is taken back and the
+        // call takes the stream path (post_and_wait)
+        const char *t = std::getenv("RSGPU_WORKER_TIMEOUT_US");
+        const long long us = t ? std::atoll(t) : 0;
+        w->timeout = std::chrono::microseconds(us > 0 ? us : 200000);
+    }
     for (int m = 0; m < 3; ++m) {
         int e = ctx->atlas_view((AtlasMode)m, w->views[m]);
         if (e) return e;
@@ -540,21 +590,15 @@ int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard
     w->enc_r = w->ver_r = (uint32_t)w->rm;
     for (int m = 0; m < 3; ++m)
         if (w->views[m].R > w->rm) return RSGPU_ERR_INVALID_ARG;  // (atlas rows per sub-pass <= min(4, p))
-    HIP_TRY(upload(er, w->d_enc));
-    HIP_TRY(upload(vr, w->d_ver));
+    HIP_TRY(upload_records(er, w->d_enc));
+    HIP_TRY(upload_records(vr, w->d_ver));
     const std::vector<uint32_t> et = record_tables(er, ctx->k, w->rm), vt = record_tables(vr, ctx->n, w->rm);
     HIP_TRY(hipMalloc(&w->d_enc_tab, et.size() * 4));
-    HIP_TRY(hipMemcpy(w->d_enc_tab, et.data(), et.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(upload(w->d_enc_tab, et.data(), et.size() * 4));
     HIP_TRY(hipMalloc(&w->d_ver_tab, vt.size() * 4));
-    HIP_TRY(hipMemcpy(w->d_ver_tab, vt.data(), vt.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(upload(w->d_ver_tab, vt.data(), vt.size() * 4));
     HIP_TRY(hipMalloc(&w->d_state, 16));
-    // a CU-masked stream is its own hardware queue: no other stream's work
-    // queues behind the resident kernel
-    int cus = 0;
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    std::vector<uint32_t> cu_mask((size_t)(cus + 31) / 32, 0xffffffffu);
-    if (cus % 32) cu_mask.back() = (1u << (cus % 32)) - 1;
-    HIP_TRY(hipExtStreamCreateWithCUMask(&w->stream, (uint32_t)cu_mask.size(), cu_mask.data()));
+    HIP_TRY(worker_stream(ctx->device, w->stream));
     HIP_TRY(hipHostMalloc((void **)&w->h_slots, sizeof(WorkerSlot) * nslots, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset((void *)w->h_slots, 0, sizeof(WorkerSlot) * nslots);
     for (int i = 0; i < nslots; ++i) w->h_slots[i].resp.exited = 1;  // generation 1: not running
@@ -572,6 +616,8 @@ int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard
     return RSGPU_OK;
 }
 
+uint64_t all_slots(const Worker &w) { return w.nslots >= 64 ? ~0ull : ((1ull << w.nslots) - 1); }
+
 int acquire_slot(Worker &w) {
     uint64_t m = w.free_mask.load(std::memory_order_relaxed);
     while (m) {
@@ -582,26 +628,52 @@ int acquire_slot(Worker &w) {
 }
 void release_slot(Worker &w, int i) { w.free_mask.fetch_or(1ull << i, std::memory_order_release); }
 
+// every granule of slot s's request line: payload rq[g], tag `tag`
+void post_line(WorkerSlot &s, const uint32_t (&rq)[8], uint32_t tag) {
+    for (int g = 0; g < 8; ++g)
+        __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
+}
+
 // Posts request `rq` (payloads) on slot i and waits for its response;
 // relaunches the resident kernel when it had left (idle) before serving it.
+// Returns RSGPU_OK (status set), kWorkerDeclined (the request was taken back
+// before any workgroup could have read it: the caller takes the stream
+// path) or an error.
+//
+// Waiting: a spin of ~50 us (a request is answered in ~7-10 us), then
+// yields, then 20 us sleeps, so a slow answer does not burn a core.
+//
+// Deadline (w.timeout, 200 ms by default): a request whose slot has no
+// workgroup of the current launch polling it yet (its launch is waiting for
+// CUs behind other work) is taken back: the tags are rewound to the last
+// number served, which no workgroup accepts, and the start mark is read
+// again.  Each workgroup writes its mark and fences before its first poll of
+// the line, and the caller fences between rewinding the tags and reading the
+// mark, so a mark still absent means no poll of this launch has read the
+// request: the call is declined and the caller's buffers are its own again.
+// A mark that appeared meanwhile means the workgroup may hold the request,
+// so it is posted again (the same number and payloads: served once either
+// way) and waited for.  A request whose workgroup is running is never taken
+// back — it would write into buffers the caller may have freed — and is
+// answered in microseconds; a kernel that dies is caught by hipStreamQuery.
 int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
+    using clk = std::chrono::steady_clock;
     WorkerSlot &s = w.h_slots[i];
     const uint32_t n = ++w.seq[i];
-    for (int g = 0; g < 8; ++g)
-        __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)n << 32), __ATOMIC_RELEASE);
-    // a call that fails takes its request back (tags of the last number
-    // served, which no workgroup accepts) and rewinds the slot's count: the
-    // caller's buffers may be gone by the time a later launch polls the slot
-    auto retract = [&](int err) {
-        for (int g = 0; g < 8; ++g)
-            __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)(n - 1) << 32), __ATOMIC_RELEASE);
+    post_line(s, rq, n);
+    auto retract = [&] {
+        post_line(s, rq, n - 1);
         --w.seq[i];
+    };
+    auto fail = [&](int err) {
+        retract();
         return err;
     };
     uint32_t cur = w.gen.load(std::memory_order_acquire);
-    const auto t_post = std::chrono::steady_clock::now();
-    unsigned spins = 0;
-    for (;;) {
+    const auto t_post = clk::now();
+    auto t_deadline = t_post + w.timeout;
+    auto t_query = t_post + std::chrono::milliseconds(1);
+    for (uint64_t spins = 1;; ++spins) {
         const uint64_t d = __atomic_load_n(&s.resp.done, __ATOMIC_ACQUIRE);
         if ((uint32_t)d == n) {
             status = (uint32_t)(d >> 32);
@@ -609,31 +681,140 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
                 auto &tr = w.tr[rq[kWfOp]];
                 tr[0].fetch_add(1);
                 for (int j = 0; j < 5; ++j) tr[1 + j].fetch_add(s.resp.pad[j]);
-                tr[6].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                    std::chrono::steady_clock::now() - t_post).count());
+                tr[6].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t_post).count());
             }
             return RSGPU_OK;
         }
         if (__atomic_load_n(&s.resp.exited, __ATOMIC_ACQUIRE) == cur) {
-            // this slot's workgroup of launch `cur` is gone (idle, or never
-            // launched): the request line stays posted, a new launch serves it
+            // this slot's workgroup of launch `cur` is gone (idle, parked, or
+            // never launched): the request line stays posted, a new launch serves it
             std::lock_guard<std::mutex> l(w.mu);
             if (w.gen.load() == cur) {
                 // every workgroup of `cur` leaves promptly
                 hipError_t he = hipStreamSynchronize(w.stream);
-                if (he != hipSuccess) return retract(hip_fail(he, "resident worker"));
-                if ((he = launch(w, cur + 1)) != hipSuccess) return retract(hip_fail(he, "resident worker launch"));
+                if (he != hipSuccess) return fail(hip_fail(he, "resident worker"));
+                if ((he = launch(w, cur + 1)) != hipSuccess) return fail(hip_fail(he, "resident worker launch"));
                 w.gen.store(cur + 1, std::memory_order_release);
                 w.launches.fetch_add(1, std::memory_order_relaxed);
             }
             cur = w.gen.load(std::memory_order_acquire);
+            t_deadline = clk::now() + w.timeout;  // (the new launch gets the whole period to start)
             continue;
         }
-        if ((++spins & 0xfffffu) == 0) {  // a kernel that died without answering
+        if (spins & 15u) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        const auto now = clk::now();
+        const auto waited = now - t_post;
+        if (waited > std::chrono::milliseconds(2)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else if (waited > std::chrono::microseconds(50)) std::this_thread::yield();
+        if (now >= t_query) {  // a kernel that died without answering
+            t_query = now + std::chrono::milliseconds(1);
             const hipError_t q = hipStreamQuery(w.stream);
-            if (q != hipSuccess && q != hipErrorNotReady) return retract(hip_fail(q, "resident worker"));
+            if (q != hipSuccess && q != hipErrorNotReady) return fail(hip_fail(q, "resident worker"));
+        }
+        if (now >= t_deadline) {
+            cur = w.gen.load(std::memory_order_acquire);
+            if (__atomic_load_n(&s.resp.started, __ATOMIC_ACQUIRE) != cur) {
+                retract();
+                std::atomic_thread_fence(std::memory_order_seq_cst);
+                if (__atomic_load_n(&s.resp.started, __ATOMIC_ACQUIRE) != cur &&
+                    (uint32_t)__atomic_load_n(&s.resp.done, __ATOMIC_ACQUIRE) != n) {
+                    w.retracted.fetch_add(1, std::memory_order_relaxed);
+                    return kWorkerDeclined;
+                }
+                ++w.seq[i];  // == n again
+                post_line(s, rq, n);
+            }
+            t_deadline = now + w.timeout;
         }
     }
+}
+
+// Takes every mailbox (calls in flight finish first; w.closed / w.parked
+// make later calls decline), then ends the resident launch and waits for it.
+// The mailboxes stay taken: a stop keeps them, a park gives them back.
+int quiesce(Worker &w) {
+    const uint64_t all = all_slots(w);
+    uint64_t got = 0;
+    while (got != all) {
+        const int i = acquire_slot(w);
+        if (i >= 0) got |= 1ull << i;
+        else std::this_thread::yield();
+    }
+    std::lock_guard<std::mutex> l(w.mu);
+    const uint32_t cur = w.gen.load();
+    if (__atomic_load_n(&w.h_slots[0].resp.exited, __ATOMIC_ACQUIRE) != cur) {
+        // running (or its launch pending): a stop request on slot 0; its
+        // workgroup raises `closing` and every other one leaves on its next
+        // poll (the other mailboxes' request numbers stay as they are)
+        WorkerSlot &s = w.h_slots[0];
+        const uint32_t n = ++w.seq[0];
+        for (int g = 0; g < 8; ++g)
+            __atomic_store_n(&s.req.g[g], (uint64_t)(g == kWfOp ? 0xffu : 0u) | ((uint64_t)n << 32), __ATOMIC_RELEASE);
+    }
+    const hipError_t he = hipStreamSynchronize(w.stream);
+    return he == hipSuccess ? RSGPU_OK : hip_fail(he, "worker stop");
+}
+
+void print_trace(Worker &w) {
+    static const char *names[6] = {"encode", "encode+verify", "verify", "reconstruct", "reconstruct-data", "decode"};
+    for (int op = 0; op < 6; ++op) {
+        const uint64_t nreq = w.tr[op][0].load();
+        if (!nreq) continue;
+        auto avg = [&](int j, double unit) { return w.tr[op][j].load() * unit / nreq; };
+        std::fprintf(stderr,
+                     "rsgpu worker trace %-16s %7llu requests; avg us after the request was seen: inputs "
+                     "loaded %.2f, computed %.2f, stores done %.2f, read back %.2f, response %.2f; host post -> "
+                     "response %.2f\n",
+                     names[op], (unsigned long long)nreq, avg(1, 0.01), avg(2, 0.01), avg(3, 0.01), avg(4, 0.01),
+                     avg(5, 0.01), avg(6, 0.001));
+    }
+}
+
+// Contexts with a worker: for parking (every worker of the process) and for
+// the process-exit guard — a resident kernel still polling when the HIP
+// runtime tears down would read freed pinned mailboxes (a GPU memory fault),
+// and a Go or C host that exits without rsgpu_destroy is normal.  The guard
+// is registered with atexit after the HIP runtime has initialised (its own
+// teardown was registered before), so it runs first and stops every worker.
+std::mutex g_live_mu;
+std::set<rsgpu_ctx *> g_live;
+// parks, starts and stops one at a time (each takes every mailbox of the
+// workers it touches; two of them interleaving would each hold a part)
+std::mutex g_park_mu;
+
+void stop_all_workers() {
+    std::vector<rsgpu_ctx *> live;
+    {
+        std::lock_guard<std::mutex> l(g_live_mu);
+        live.assign(g_live.begin(), g_live.end());
+    }
+    for (rsgpu_ctx *c : live) (void)rsgpu_worker_stop(c);
+}
+void track_worker(rsgpu_ctx *ctx, bool on) {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(stop_all_workers); });
+    std::lock_guard<std::mutex> l(g_live_mu);
+    if (on) g_live.insert(ctx);
+    else g_live.erase(ctx);
+}
+
+// ctx's worker stopped and detached (ctx->worker_mu and g_park_mu held)
+int stop_locked(rsgpu_ctx *ctx) {
+    std::shared_ptr<Worker> w = std::atomic_exchange(&ctx->worker, std::shared_ptr<Worker>());
+    track_worker(ctx, false);
+    if (!w) return RSGPU_OK;
+    w->closed.store(true, std::memory_order_release);
+    DeviceGuard dg_;
+    int e = ctx->use_device(dg_, false);
+    if (!e) e = quiesce(*w);
+    if (w->trace) print_trace(*w);
+    // its kernel has left: what was retired while it ran may be freed now
+    // (calls still holding `w` are declined; the last reference frees it)
+    worker_count(-1);
+    return e;
 }
 
 }  // namespace
@@ -641,7 +822,10 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
 // The worker serves one object when it can: returns RSGPU_OK with *bad set
 // (0 / 1), kWorkerDeclined to use the stream path, or an error.
 int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *const *rows, uint32_t *bad) {
-    Worker *w = ctx->worker.get();
+    // a reference: a concurrent rsgpu_worker_stop detaches the worker, and
+    // its memory lives until this call is done with it
+    const std::shared_ptr<Worker> ref = std::atomic_load(&ctx->worker);
+    Worker *w = ref.get();
     if (!w || S > w->max_shard || S == 0) return kWorkerDeclined;
     const int n = ctx->n, k = ctx->k;
     const uint32_t full = (1u << n) - 1;
@@ -653,7 +837,11 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
         case kWopReconstructData: rd = mask; wr = ~mask & ((1u << k) - 1); break;
         default: rd = mask; wr = ~mask & full; break;
     }
-    const int i = acquire_slot(*w);
+    // stopped or parked: decline (checked before and after taking a mailbox;
+    // a stop / park takes every mailbox, so one of the two checks sees it)
+    const int i = w->closed.load(std::memory_order_acquire) || w->parked.load(std::memory_order_acquire)
+                      ? -1
+                      : acquire_slot(*w);
     if (i < 0) {  // every mailbox busy: the stream path takes this call
         w->declined.fetch_add(1, std::memory_order_relaxed);
         return kWorkerDeclined;
@@ -677,82 +865,41 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
         for (int r = 0; r < n; ++r)
             if ((wr >> r) & 1) std::memcpy(rows[r], w->stage_h[i] + (size_t)r * S, S);
     release_slot(*w, i);
+    if (e == kWorkerDeclined) {
+        w->declined.fetch_add(1, std::memory_order_relaxed);
+        return kWorkerDeclined;
+    }
     if (e) return e;
     w->served.fetch_add(1, std::memory_order_relaxed);
     *bad = status;
     return RSGPU_OK;
 }
 
-int worker_stop(rsgpu_ctx *ctx) {
-    Worker *w = ctx->worker.get();
-    if (!w) return RSGPU_OK;
-    // take every mailbox (calls in flight finish first), then one stop request
-    const uint64_t all = w->nslots >= 64 ? ~0ull : ((1ull << w->nslots) - 1);
-    uint64_t got = 0;
-    while (got != all) {
-        const int i = acquire_slot(*w);
-        if (i >= 0) got |= 1ull << i;
-        else std::this_thread::yield();
+int with_workers_parked(const std::function<int()> &fn) {
+    std::lock_guard<std::mutex> pl(g_park_mu);
+    std::vector<std::shared_ptr<Worker>> ws;
+    {
+        std::lock_guard<std::mutex> l(g_live_mu);
+        for (rsgpu_ctx *c : g_live)
+            if (auto w = std::atomic_load(&c->worker)) ws.push_back(std::move(w));
     }
-    std::lock_guard<std::mutex> l(w->mu);
-    const uint32_t cur = w->gen.load();
-    if (__atomic_load_n(&w->h_slots[0].resp.exited, __ATOMIC_ACQUIRE) != cur) {
-        // running: a stop request on slot 0; its workgroup raises `closing`
-        // and every other one leaves on its next poll (the other mailboxes'
-        // request numbers stay as they are)
-        WorkerSlot &s = w->h_slots[0];
-        const uint32_t n = ++w->seq[0];
-        for (int g = 0; g < 8; ++g)
-            __atomic_store_n(&s.req.g[g], (uint64_t)(g == kWfOp ? 0xffu : 0u) | ((uint64_t)n << 32), __ATOMIC_RELEASE);
-    }
+    if (ws.empty()) return fn();
     int e = RSGPU_OK;
-    const hipError_t he = hipStreamSynchronize(w->stream);
-    if (he != hipSuccess) e = hip_fail(he, "worker stop");
-    w->free_mask.store(all);
-    if (w->trace) {
-        static const char *names[6] = {"encode", "encode+verify", "verify", "reconstruct", "reconstruct-data", "decode"};
-        for (int op = 0; op < 6; ++op) {
-            const uint64_t nreq = w->tr[op][0].load();
-            if (!nreq) continue;
-            auto avg = [&](int j, double unit) { return w->tr[op][j].load() * unit / nreq; };
-            std::fprintf(stderr,
-                         "rsgpu worker trace %-16s %7llu requests; avg us after the request was seen: inputs "
-                         "loaded %.2f, computed %.2f, stores done %.2f, read back %.2f, response %.2f; host post -> "
-                         "response %.2f\n",
-                         names[op], (unsigned long long)nreq, avg(1, 0.01), avg(2, 0.01), avg(3, 0.01), avg(4, 0.01),
-                         avg(5, 0.01), avg(6, 0.001));
-        }
+    for (auto &w : ws) {
+        w->parked.fetch_add(1, std::memory_order_acq_rel);
+        const int q = quiesce(*w);
+        if (!e) e = q;
     }
-    return e;
+    const int r = fn();
+    if (!e) drain_retired();  // no worker kernel is resident: the kept buffers go too
+    for (auto &w : ws) {
+        w->free_mask.store(all_slots(*w), std::memory_order_release);
+        w->parked.fetch_sub(1, std::memory_order_acq_rel);
+    }
+    return e ? e : r;
 }
 
 }  // namespace rsgpu
-
-// Contexts with a worker, for the process-exit guard: a resident kernel
-// still polling when the HIP runtime tears down would read freed pinned
-// mailboxes (a GPU memory fault), and a Go or C host that exits without
-// rsgpu_destroy is normal.  The guard is registered with atexit after the
-// HIP runtime has initialised (its own teardown was registered before), so
-// it runs first and stops every worker.
-namespace {
-std::mutex g_live_mu;
-std::set<rsgpu_ctx *> g_live;
-void stop_all_workers() {
-    std::vector<rsgpu_ctx *> live;
-    {
-        std::lock_guard<std::mutex> l(g_live_mu);
-        live.assign(g_live.begin(), g_live.end());
-    }
-    for (rsgpu_ctx *c : live) (void)rsgpu_worker_stop(c);
-}
-void track_worker(rsgpu_ctx *ctx, bool on) {
-    static std::once_flag once;
-    std::call_once(once, [] { std::atexit(stop_all_workers); });
-    std::lock_guard<std::mutex> l(g_live_mu);
-    if (on) g_live.insert(ctx);
-    else g_live.erase(ctx);
-}
-}  // namespace
 
 // ============================================================== C ABI
 
@@ -761,9 +908,12 @@ extern "C" {
 int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard) {
     if (!ctx || nslots < 0 || nslots > 64) return RSGPU_ERR_INVALID_ARG;
     if (ctx->multi()) {
-        for (auto &c : ctx->subs) {
-            const int e = rsgpu_worker_start(c.get(), nslots, idle_us, max_shard);
-            if (e) return e;
+        for (size_t i = 0; i < ctx->subs.size(); ++i) {
+            const int e = rsgpu_worker_start(ctx->subs[i].get(), nslots, idle_us, max_shard);
+            if (e) {  // no entry is left with a worker
+                for (size_t j = 0; j < i; ++j) (void)rsgpu_worker_stop(ctx->subs[j].get());
+                return e;
+            }
         }
         return RSGPU_OK;
     }
@@ -774,16 +924,15 @@ int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_
     if (!max_shard) max_shard = 4096;  // worker ahead of the stream path up to ~40 KB objects (r03_lat_*_sizes.txt)
     if (max_shard > ((size_t)1 << 24)) return RSGPU_ERR_INVALID_ARG;
     DeviceGuard dg_;
-    int e = ctx->use_device(dg_);
+    int e = ctx->use_device(dg_, false);
     if (e) return e;
     std::lock_guard<std::mutex> l(ctx->worker_mu);
-    if (ctx->worker) {  // restart with the new settings
-        if ((e = worker_stop(ctx))) return e;
-        ctx->worker.reset();
-    }
+    std::lock_guard<std::mutex> pl(g_park_mu);
+    if ((e = stop_locked(ctx))) return e;  // restart with the new settings
     std::unique_ptr<Worker> w;
     if ((e = worker_create(ctx, nslots, idle_us, max_shard, w))) return e;
-    ctx->worker.reset(w.release());
+    worker_count(+1);  // before its first launch (the first request's)
+    std::atomic_store(&ctx->worker, std::shared_ptr<Worker>(w.release()));
     track_worker(ctx, true);
     return RSGPU_OK;
 }
@@ -792,7 +941,7 @@ int rsgpu_worker_stats(const rsgpu_ctx *ctx, uint64_t *served, uint64_t *decline
     if (!ctx) return RSGPU_ERR_INVALID_ARG;
     uint64_t s = 0, d = 0, l = 0;
     auto add = [&](const rsgpu_ctx *c) {
-        if (const Worker *w = c->worker.get()) {
+        if (const std::shared_ptr<Worker> w = std::atomic_load(&c->worker)) {
             s += w->served.load();
             d += w->declined.load();
             l += w->launches.load();
@@ -817,16 +966,8 @@ int rsgpu_worker_stop(rsgpu_ctx *ctx) {
         return first;
     }
     std::lock_guard<std::mutex> l(ctx->worker_mu);
-    if (!ctx->worker) {
-        track_worker(ctx, false);  // (a restart whose create failed left it listed)
-        return RSGPU_OK;
-    }
-    DeviceGuard dg_;
-    int e = ctx->use_device(dg_);
-    if (!e) e = worker_stop(ctx);
-    ctx->worker.reset();
-    track_worker(ctx, false);
-    return e;
+    std::lock_guard<std::mutex> pl(g_park_mu);
+    return stop_locked(ctx);
 }
 
 }  // extern "C"

@@ -58,10 +58,10 @@ int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
     for (auto &s : P.slots) {
         if (s->cap >= bytes) continue;
         HIP_TRY(hipStreamSynchronize(s->stream));
-        if (s->d) (void)hipFree(s->d);
+        retire(s->d, false);  // (freed once no worker runs: devmem.cpp)
+        const size_t cap = round_up(std::max(bytes, s->cap + s->cap / 2), (size_t)1 << 20);
         s->d = nullptr;
         s->cap = 0;
-        const size_t cap = round_up(bytes, (size_t)1 << 20);
         HIP_TRY(hipMalloc(&s->d, cap));
         s->cap = cap;
     }
@@ -71,11 +71,12 @@ int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
 int ensure_flags(rsgpu_ctx *ctx, int nobj) {
     auto &P = ctx->pipe;
     if (P.h_bad_cap >= (size_t)nobj) return RSGPU_OK;
-    if (P.h_bad) (void)hipHostFree(P.h_bad);
+    retire(P.h_bad, true);
+    const size_t cap = std::max<size_t>({(size_t)nobj, 1, P.h_bad_cap * 2});
     P.h_bad = nullptr;
     P.h_bad_cap = 0;
-    HIP_TRY(hipHostMalloc(&P.h_bad, (size_t)std::max(nobj, 1) * 4, hipHostMallocDefault));
-    P.h_bad_cap = (size_t)std::max(nobj, 1);
+    HIP_TRY(hipHostMalloc(&P.h_bad, cap * 4, hipHostMallocDefault));
+    P.h_bad_cap = cap;
     return RSGPU_OK;
 }
 
@@ -150,11 +151,18 @@ int rsgpu_host_register(void *p, size_t len) {
     return RSGPU_OK;
 }
 
+// hipHostUnregister / hipHostFree synchronise the device
+// (profiles/r04_sync_probe*.txt): with a resident worker they would wait
+// until it idles out, so every worker is parked around them
+// (with_workers_parked: calls in flight finish, later ones take the stream
+// path, the next one relaunches).
 int rsgpu_host_unregister(void *p) {
     if (!p) return RSGPU_ERR_INVALID_ARG;
     pin_del(p);
-    HIP_TRY(hipHostUnregister(p));
-    return RSGPU_OK;
+    return with_workers_parked([p] {
+        HIP_TRY(hipHostUnregister(p));
+        return RSGPU_OK;
+    });
 }
 
 int rsgpu_host_alloc(size_t len, void **out) {
@@ -171,8 +179,10 @@ int rsgpu_host_alloc(size_t len, void **out) {
 int rsgpu_host_free(void *p) {
     if (!p) return RSGPU_OK;
     pin_del(p);
-    HIP_TRY(hipHostFree(p));
-    return RSGPU_OK;
+    return with_workers_parked([p] {
+        HIP_TRY(hipHostFree(p));
+        return RSGPU_OK;
+    });
 }
 
 }  // extern "C"

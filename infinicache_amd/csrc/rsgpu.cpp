@@ -403,11 +403,11 @@ int build_atlas_host(rsgpu_ctx *ctx, AtlasMode mode, Atlas &A) {
 // into D, this context's device copy.  On failure nothing stays allocated.
 int upload_atlas(rsgpu_ctx *ctx, const Atlas &H, Atlas &D) {
     hipError_t e = hipMalloc(&D.d_pat, H.h_pat.size() * 4);
-    if (e == hipSuccess) e = hipMemcpy(D.d_pat, H.h_pat.data(), H.h_pat.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload(D.d_pat, H.h_pat.data(), H.h_pat.size() * 4);
     if (e == hipSuccess) e = hipMalloc(&D.d_recs, H.h_recs.size());
-    if (e == hipSuccess) e = hipMemcpy(D.d_recs, H.h_recs.data(), H.h_recs.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload(D.d_recs, H.h_recs.data(), H.h_recs.size());
     if (e == hipSuccess) e = hipMalloc(&D.d_tabs, H.h_tabs.size() * 4);
-    if (e == hipSuccess) e = hipMemcpy(D.d_tabs, H.h_tabs.data(), H.h_tabs.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload(D.d_tabs, H.h_tabs.data(), H.h_tabs.size() * 4);
     if (e != hipSuccess) {
         D.free_dev();
         return hip_fail(e, "atlas upload");
@@ -484,9 +484,9 @@ int rsgpu_ctx::atlas_view(AtlasMode mode, AtlasView &out) {
             for (int c = 0; c < 256; ++c) coef_tables((uint8_t)c, &t[(size_t)c * kCtabStride]);
             uint32_t *d = nullptr;
             hipError_t he = hipMalloc(&d, t.size() * 4);
-            if (he == hipSuccess) he = hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+            if (he == hipSuccess) he = upload(d, t.data(), t.size() * 4);
             if (he != hipSuccess) {
-                if (d) (void)hipFree(d);
+                retire(d, false);
                 return hip_fail(he, "atlas coefficient table");  // retried by the next call
             }
             d_ctab = d;
@@ -574,7 +574,10 @@ int dev_masks_host(rsgpu_ctx *ctx, const Layout &L, const uint32_t *d_masks, Atl
     }
     // statuses of the objects no launch touches; the coded ones start at 0
     // and the check rows raise theirs to 1
-    if (d_status) HIP_TRY(hipMemcpy(d_status, status.data(), (size_t)nobj * 4, hipMemcpyHostToDevice));
+    if (d_status) {  // on the call's stream (ordered with its launches), never the null stream
+        HIP_TRY(hipMemcpyAsync(d_status, status.data(), (size_t)nobj * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));  // `status` is a local
+    }
     if (plans.empty()) return RSGPU_OK;
     HIP_TRY(launch_plans_multi(plans, plan_of, L, check ? d_status : nullptr, st, ctx->multi_ws));
     return RSGPU_OK;
@@ -821,7 +824,7 @@ static int reconstruct_common(rsgpu_ctx *ctx, uint8_t *const *shards, const size
         if (!shards[plan->out_rows[r]]) return RSGPU_ERR_INVALID_ARG;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
-    if (ctx->worker) {
+    if (std::atomic_load(&ctx->worker)) {
         // the worker writes every missing row it rebuilds through rows[i]:
         // each needs a buffer (ReconstructData: the missing data rows only)
         bool bufs = true;
@@ -1125,8 +1128,8 @@ static int recon_dev_multi_atlas(rsgpu_ctx *ctx, void *d_base, const uint8_t *pr
     else HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     const size_t bytes = (size_t)nobj * 4;
     if (w.cap < bytes) {
-        if (w.d) (void)hipFree(w.d);
-        if (w.h) (void)hipHostFree(w.h);
+        retire(w.d, false);  // (freed once no worker runs: devmem.cpp)
+        retire(w.h, true);
         w.d = nullptr;
         w.h = nullptr;
         w.cap = 0;

@@ -421,6 +421,15 @@ class RSEncoder:
                                                    _stream_handle(stream)))
 
     # -- batched host-memory API (pipelined H2D -> kernel -> D2H) ----------
+    def copy_pieces(self, src, src_pitch, src_obj_stride, dst, dst_pitch, dst_obj_stride, shard_len, nobj,
+                    rows=None, stream=None):
+        """rsgpu_copy_pieces: move rows `rows` (row indices; default every
+        row) of nobj objects between two device layouts (object-major or
+        shard-major), exactly shard_len bytes per piece."""
+        mask = (1 << self.Shards) - 1 if rows is None else sum(1 << int(i) for i in rows)
+        _check(self._L.rsgpu_copy_pieces(self._ctx, _dptr(src), src_pitch, src_obj_stride, _dptr(dst), dst_pitch,
+                                         dst_obj_stride, shard_len, nobj, mask, _stream_handle(stream)))
+
     def encode_batch(self, objs: Sequence) -> None:
         """Encode many objects, each given as its Split() result (or the
         backing array of one): parity rows are written in place.  Host
@@ -488,6 +497,16 @@ class RSEncoder:
         ok = (ctypes.c_int * max(nobj, 1))()
         _check(self._L.rsgpu_decode_batch(self._ctx, ptrs, pres, lens, nobj, ok))
         return [bool(ok[o]) for o in range(nobj)]
+
+
+def shardmajor_layout(shard_len: int, nobj: int):
+    """rsgpu_shardmajor_layout: (obj_stride, pitch) of a shard-major batch of
+    nobj pieces of shard_len bytes on whole 128-B lines (when the gap stays
+    at most shard_len / 4; else 16-B aligned pieces)."""
+    L = _lib.load()
+    st, pi = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(L.rsgpu_shardmajor_layout(shard_len, nobj, ctypes.byref(st), ctypes.byref(pi)))
+    return st.value, pi.value
 
 
 def host_alloc(nbytes: int) -> np.ndarray:

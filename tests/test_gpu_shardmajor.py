@@ -239,3 +239,97 @@ def test_shard_major_masks_vs_oracle(gpu, k, p, S, nobj, op):
             assert st[o] == (0 if okv else 1), (o, present[o])
         else:
             assert st[o] == 0, o
+
+
+def _obj_major_golden(k, p, S, nobj, seed):
+    """nobj objects' n rows (data random, parity from the oracle), (nobj, n, S)."""
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, (nobj, k, S), dtype=np.uint8)
+    m = ia.New(k, p).matrix()
+    # coding is byte-position-wise: every object's row c back to back is one long row
+    par = oracle.apply(m[k:], [np.ascontiguousarray(data[:, c, :]).reshape(-1) for c in range(k)])
+    full = np.empty((nobj, k + p, S), np.uint8)
+    full[:, :k] = data
+    for r in range(p):
+        full[:, k + r] = np.frombuffer(bytes(par[r]), np.uint8).reshape(nobj, S)
+    return full
+
+
+@pytest.mark.parametrize("k,p,S,nobj,src_align", [(10, 2, 103, 3000, 1), (10, 2, 103, 2000, 16), (10, 4, 410, 500, 16),
+                                                  (6, 3, 1000, 64, 1), (10, 2, 17, 700, 1), (10, 2, 4099, 40, 256),
+                                                  (12, 4, 128, 300, 128)])
+def test_shardmajor_helper_get_batch_vs_oracle(gpu, k, p, S, nobj, src_align):
+    """a Get batch arrives object-major (each object's
+    bodies back to back, any pitch), rsgpu_copy_pieces moves it into the
+    library's whole-line shard-major layout (rsgpu_shardmajor_layout), the
+    per-object patterns are decoded there (*_dev_masks) and the rows come
+    back object-major: bit-exact against the oracle, pad bytes of the
+    destination untouched (every piece copy writes exactly shard_len bytes)."""
+    n = k + p
+    stride, pitch = ia.shardmajor_layout(S, nobj)
+    assert stride % 16 == 0 and pitch % 256 == 0 and pitch >= nobj * stride >= nobj * S
+    whole = (-S % 128) * 4 <= S
+    assert (stride % 128 == 0) == whole or stride == (S + 15) // 16 * 16
+    full = _obj_major_golden(k, p, S, nobj, seed=S * 7 + nobj)
+    sp = (S + src_align - 1) // src_align * src_align
+    src = torch.zeros((nobj, n, sp), dtype=torch.uint8, device="cuda")
+    src[:, :, :S] = torch.from_numpy(full).to("cuda")
+    sm = torch.full((n, pitch), 0x77, dtype=torch.uint8, device="cuda")
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    enc.copy_pieces(src, sp, n * sp, sm, pitch, stride, S, nobj, stream=s)
+    torch.cuda.synchronize()
+    pieces = sm[:, :nobj * stride].view(n, nobj, stride)
+    assert torch.equal(pieces[:, :, :S].permute(1, 0, 2).cpu(), torch.from_numpy(full))
+    if stride > S:  # gaps untouched by the copy
+        assert bool((pieces[:, :, S:] == 0x77).all())
+    # per-object erasures (0..p lost, first-d rule on the survivors), lost pieces garbage
+    rng = np.random.default_rng(nobj + S)
+    present = np.ones((nobj, n), np.uint8)
+    for o in range(nobj):
+        present[o, rng.choice(n, int(rng.integers(0, p + 1)), replace=False)] = 0
+    lost = torch.from_numpy(present == 0).to("cuda")  # (nobj, n)
+    pv = pieces.permute(1, 0, 2)  # (nobj, n, stride) view
+    pv[..., :S][lost] = 0xA5
+    masks = (present.astype(np.int64) * (1 << np.arange(n, dtype=np.int64))).sum(axis=1).astype(np.uint32)
+    dmask = torch.from_numpy(masks.view(np.int32)).to("cuda")
+    status = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    enc.decode_dev_masks(sm, dmask, S, pitch, stride, nobj, status, s)
+    out = torch.zeros((nobj, n, sp), dtype=torch.uint8, device="cuda")
+    if sp > S:
+        out[:, :, S:] = 0x3C
+    enc.copy_pieces(sm, pitch, stride, out, sp, n * sp, S, nobj, stream=s)
+    torch.cuda.synchronize()
+    assert int(status.abs().sum().item()) == 0, np.flatnonzero(status.cpu().numpy())[:5]
+    assert np.array_equal(out[:, :, :S].cpu().numpy(), full)
+    if sp > S:
+        assert bool((out[:, :, S:] == 0x3C).all())
+
+
+@pytest.mark.parametrize("S,nobj,rows", [(1, 1, (0,)), (103, 777, (1, 5, 11)), (4099, 33, (0, 11)),
+                                         (17, 4000, tuple(range(12))), (1000, 3, (2, 3))])
+def test_copy_pieces_exact_rows_both_ways(gpu, S, nobj, rows):
+    """Only the listed rows' shard_len bytes move, at odd strides both ways
+    (object-major byte-packed <-> shard-major at an unaligned stride)."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    g = torch.Generator(device="cuda").manual_seed(S + nobj)
+    src = torch.randint(0, 256, (nobj, n, S), dtype=torch.uint8, device="cuda", generator=g)  # byte-packed
+    ds = S + 3  # unaligned stride
+    dp = nobj * ds + 5
+    dst = torch.full((n, dp), 0x11, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    enc.copy_pieces(src, S, n * S, dst, dp, ds, S, nobj, rows=rows, stream=s)
+    back = torch.full((nobj, n, S + 1), 0x22, dtype=torch.uint8, device="cuda")
+    enc.copy_pieces(dst, dp, ds, back, S + 1, n * (S + 1), S, nobj, rows=rows, stream=s)
+    torch.cuda.synchronize()
+    want = torch.full((n, dp), 0x11, dtype=torch.uint8)
+    h = src.cpu()
+    for i in rows:
+        want[i, :nobj * ds].view(nobj, ds)[:, :S] = h[:, i]
+    assert torch.equal(dst.cpu(), want)
+    wb = torch.full((nobj, n, S + 1), 0x22, dtype=torch.uint8)
+    for i in rows:
+        wb[:, i, :S] = h[:, i]
+    assert torch.equal(back.cpu(), wb)

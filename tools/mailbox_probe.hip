@@ -71,8 +71,15 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p) {
 // waited to poll: a kernel that never ends.  So the whole of wave 0 polls,
 // every polled value goes through readfirstlane (scalar), and the request
 // number reaches the other waves through LDS + readfirstlane.
+// Round 4: the pointers and S the kernel rebuilds from
+// the mailbox are recorded in mb->pad2 (system-scope stores, completed with
+// vmcnt(0) before any row access, so they reach the host even if a row
+// access then faults) and compared with the values the host passed as kernel
+// arguments; on a mismatch the kernel flags it (pad2[6]) and answers the
+// request without touching a row.
 template <int VARIANT, int SLEEP>
-__global__ __launch_bounds__(256) void worker(Mailbox *mb, uint32_t *bell, uint64_t idle_ticks) {
+__global__ __launch_bounds__(256) void worker(Mailbox *mb, uint32_t *bell, uint64_t idle_ticks, uint64_t want_in,
+                                              uint64_t want_out, uint32_t want_S) {
     __shared__ uint32_t s_seq;
     const uint32_t t = threadIdx.x;
     uint32_t last = 0;
@@ -102,6 +109,17 @@ __global__ __launch_bounds__(256) void worker(Mailbox *mb, uint32_t *bell, uint6
         uint8_t *out = (uint8_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(outp >> 32)) << 32) |
                                    __builtin_amdgcn_readfirstlane((uint32_t)outp));
         const uint32_t nvec = (S + 15) / 16;
+        const bool same = (uint64_t)in == want_in && (uint64_t)out == want_out && S == want_S;
+        if (t == 0) {
+            uint32_t rec[7] = {S, (uint32_t)(uint64_t)in, (uint32_t)((uint64_t)in >> 32), (uint32_t)(uint64_t)out,
+                               (uint32_t)((uint64_t)out >> 32), s, same ? 0u : 1u};
+            for (int i = 0; i < 7; ++i) __hip_atomic_store(&mb->pad2[i], rec[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (!__syncthreads_and(same)) {  // never dereference a pointer the host did not pass
+            if (t == 0) __hip_atomic_store(&mb->resp, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+        }
         const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)(12 * S + 64), 0x00020000);
         const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)(2 * nvec * 16), 0x00020000);
         if (t < nvec) {
@@ -194,17 +212,29 @@ static void run_poll(const char *name, bool devbell, int iters) {
     }
     const uint32_t S = 103;
     uint8_t *in = nullptr, *out = nullptr, *din = nullptr, *dout = nullptr;
-    CK(hipHostMalloc((void **)&in, 12 * S + 64, hipHostMallocDefault));
-    CK(hipHostMalloc((void **)&out, 2 * 112 + 64, hipHostMallocDefault));
+    // PROBE_ROWS_COHERENT=1: the rows as the product worker's images
+    // (Mapped | Coherent); default: hipHostMallocDefault (the r03 run)
+    const unsigned rflags = std::getenv("PROBE_ROWS_COHERENT") ? (hipHostMallocMapped | hipHostMallocCoherent)
+                                                               : hipHostMallocDefault;
+    CK(hipHostMalloc((void **)&in, 12 * S + 64, rflags));
+    CK(hipHostMalloc((void **)&out, 2 * 112 + 64, rflags));
     CK(hipHostGetDevicePointer((void **)&din, in, 0));
     CK(hipHostGetDevicePointer((void **)&dout, out, 0));
+    for (int i = 0; i < 2; ++i) {
+        hipPointerAttribute_t at;
+        const void *hp = i ? (const void *)out : (const void *)in;
+        CK(hipPointerGetAttributes(&at, hp));
+        std::printf("%s: %s host %p device %p: type %d allocationFlags 0x%x isManaged %d\n", name, i ? "out" : "in",
+                    hp, i ? (void *)dout : (void *)din, (int)at.type, at.allocationFlags, at.isManaged);
+    }
     mb->S = S;
     mb->in = (uint64_t)din;
     mb->out = (uint64_t)dout;
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     std::printf("%s: launching\n", name);
-    hipLaunchKernelGGL((worker<VARIANT, SLEEP>), dim3(1), dim3(256), 0, st, dmb, bell_dev, (uint64_t)200000000);  // 2 s idle
+    hipLaunchKernelGGL((worker<VARIANT, SLEEP>), dim3(1), dim3(256), 0, st, dmb, bell_dev, (uint64_t)200000000,
+                       (uint64_t)din, (uint64_t)dout, S);  // 2 s idle
     CK(hipGetLastError());
     std::vector<double> lat;
     int bad = 0;
@@ -226,12 +256,22 @@ static void run_poll(const char *name, bool devbell, int iters) {
             if (now_us() - t0 > 1e6) {
                 std::printf("%s: no response after 1 s at request %d (kernel started: %u)\n", name, it,
                             __atomic_load_n(&mb->pad, __ATOMIC_ACQUIRE));
+                std::printf("%s: kernel read S %u in 0x%08x%08x out 0x%08x%08x at request %u, mismatch %u "
+                            "(host passed S %u in %p out %p)\n",
+                            name, mb->pad2[0], mb->pad2[2], mb->pad2[1], mb->pad2[4], mb->pad2[3], mb->pad2[5],
+                            mb->pad2[6], S, (void *)din, (void *)dout);
                 mb->stop = 1;
                 CK(hipStreamSynchronize(st));
                 return;
             }
         }
         const double t1 = now_us();
+        if (mb->pad2[6]) {
+            std::printf("%s: request %d: the kernel read S %u in 0x%08x%08x out 0x%08x%08x, not what the host passed\n",
+                        name, it, mb->pad2[0], mb->pad2[2], mb->pad2[1], mb->pad2[4], mb->pad2[3]);
+            ++bad;
+            mb->pad2[6] = 0;
+        }
         if (std::memcmp(out, want[0], S) || std::memcmp(out + 112, want[1], S)) ++bad;
         lat.push_back(t1 - t0);
     }
@@ -279,7 +319,8 @@ static void run_direct(const char *name, int iters) {
     mb->out = (uint64_t)dout;
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    hipLaunchKernelGGL((worker<VARIANT, SLEEP>), dim3(1), dim3(256), 0, st, dmb, bell, (uint64_t)200000000);
+    hipLaunchKernelGGL((worker<VARIANT, SLEEP>), dim3(1), dim3(256), 0, st, dmb, bell, (uint64_t)200000000,
+                       (uint64_t)din, (uint64_t)dout, S);
     CK(hipGetLastError());
     std::vector<double> lat, wr;
     int bad = 0;
