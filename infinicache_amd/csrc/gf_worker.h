@@ -30,9 +30,24 @@ enum WorkerOp : uint32_t {
     kWopDecode = 5,        // fused Client.decode (atlas mode kAtlasDecode)
 };
 
-// granule payloads of a request line
-enum WorkerField { kWfOp = 0, kWfShardLen = 1, kWfMask = 2, kWfPitch = 3, kWfInLo = 4, kWfInHi = 5, kWfOutLo = 6,
+// granule payloads of a request line (rows at pitch = shard length: Split's
+// layout; kWfSum checks the other seven payloads)
+enum WorkerField { kWfOp = 0, kWfShardLen = 1, kWfMask = 2, kWfSum = 3, kWfInLo = 4, kWfInHi = 5, kWfOutLo = 6,
                    kWfOutHi = 7 };
+
+// The request line's check word.  Every granule is one aligned 8-B store,
+// which the worker accepts only once its tag is current; the check word
+// also catches a payload word that arrived apart from its tag (the VRAM
+// transport's lines are written through the write-combining BAR mapping,
+// whose flush granularity the library does not control): the worker polls
+// again until the sum matches.
+__host__ __device__ inline uint32_t worker_req_sum(const uint32_t *p) {
+    auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+    uint32_t h = 0x5bd1e995u ^ (p[kWfOp] * 0x9E3779B1u);
+    h ^= rotl(p[kWfShardLen], 7) ^ rotl(p[kWfMask], 13) ^ p[kWfInLo] ^ rotl(p[kWfInHi], 3);
+    h ^= rotl(p[kWfOutLo], 17) ^ rotl(p[kWfOutHi], 23);
+    return h * 0x85EBCA6Bu ^ (h >> 15);
+}
 
 struct alignas(64) WorkerReq {
     uint64_t g[8];  // low 32 bits: payload (WorkerField), high 32 bits: tag (request number)
@@ -52,7 +67,9 @@ static_assert(sizeof(WorkerSlot) == 128, "one line per direction");
 constexpr uint32_t kWorkerMaxN = 16;  // codes of <= 16 shards (PatRec records)
 
 struct WorkerArgs {
-    WorkerSlot *slots;          // device view of the host mailboxes
+    WorkerSlot *slots;          // device view of the host mailboxes (responses; host transport: requests too)
+    WorkerReq *vreq;            // VRAM transport: the request lines in fine-grained VRAM (else null)
+    uint32_t *vmark;            // VRAM transport: start marks, 64 B apart (else resp.started)
     const int32_t *pat[3];      // atlases by mode (kAtlasReconstruct, kAtlasData, kAtlasDecode)
     const void *recs[3];        // PatRec [slot][nsub]
     const uint32_t *tabs[3];    // [slot][nsub][tk][tr][kTabWords] v_perm tables

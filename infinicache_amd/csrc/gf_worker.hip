@@ -98,11 +98,15 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
         lt[t][1] = ct[1];
     }
     WorkerSlot *ms = a.slots + blockIdx.x;
-    // the start mark reaches host memory before this workgroup's first poll
-    // of the request line: a caller that sees no mark after taking its
-    // request back knows no poll of this launch can have read it
+    // the request line: in pinned host memory (host transport) or in
+    // fine-grained VRAM the host writes through the BAR (VRAM transport)
+    const WorkerReq *rl = a.vreq ? a.vreq + blockIdx.x : &ms->req;
+    uint32_t *mark = a.vreq ? a.vmark + blockIdx.x * 16u : &ms->resp.started;
+    // the start mark (beside the request line) is stored before this
+    // workgroup's first poll of the line: a caller that sees no mark after
+    // taking its request back knows no poll of this launch can have read it
     // (post_and_wait's deadline)
-    if (t == 0) __hip_atomic_store(&ms->resp.started, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) __hip_atomic_store(mark, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");  // store -> later loads (system scope; once per launch)
     // the last request served on this slot (by this or an earlier launch)
     uint32_t last = rfl((uint32_t)__hip_atomic_load(&ms->resp.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
@@ -118,12 +122,17 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
         uint32_t polls = 0;
         for (;;) {
             uint64_t gv = 0;
-            if (lane < 8) gv = __hip_atomic_load(&ms->req.g[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane < 8) gv = __hip_atomic_load(&rl->g[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             const bool ok = lane >= 8 || (uint32_t)(gv >> 32) == want;
             if (__builtin_amdgcn_ballot_w64(!ok) == 0) {  // all eight granules carry the number
-                if (lane < 8) sreq[lane] = (uint32_t)gv;
-                if (lane == 0) sfound = want;  // (several waves may find it: same bytes)
-                break;
+                uint32_t pl[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pl[j] = __builtin_amdgcn_readlane((uint32_t)gv, j);
+                if (worker_req_sum(pl) == pl[kWfSum]) {  // else a payload caught mid-write: poll again
+                    if (lane < 8) sreq[lane] = (uint32_t)gv;
+                    if (lane == 0) sfound = want;  // (several waves may find it: same bytes)
+                    break;
+                }
             }
             const uint32_t f = rfl(sfound);
             if (f == want || f == ~0u) break;  // another wave found it, or the launch closes
@@ -164,7 +173,7 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
             }
             return;
         }
-        const uint32_t S = rfl(sreq[kWfShardLen]), mask = rfl(sreq[kWfMask]) & a.nmask, pitch = rfl(sreq[kWfPitch]);
+        const uint32_t S = rfl(sreq[kWfShardLen]), mask = rfl(sreq[kWfMask]) & a.nmask, pitch = S;
         const uint64_t inb = (uint64_t)rfl(sreq[kWfInLo]) | ((uint64_t)rfl(sreq[kWfInHi]) << 32);
         const uint64_t outb = (uint64_t)rfl(sreq[kWfOutLo]) | ((uint64_t)rfl(sreq[kWfOutHi]) << 32);
         __syncthreads();  // sreq is rewritten by the next poll
@@ -413,6 +422,16 @@ struct Worker {
     WorkerSlot *h_slots = nullptr, *d_slots = nullptr;  // coherent pinned mailboxes
     std::vector<uint8_t *> stage_h, stage_d;            // per slot: a coherent pinned object image
     size_t stage_cap = 0;
+    // VRAM transport (RSGPU_WORKER_TRANSPORT=vram): request lines, start
+    // marks and per-slot input images in one fine-grained VRAM allocation the
+    // CPU writes through the BAR (same address on both sides); the input
+    // rows are copied there, so the kernel's poll and its row loads stay on
+    // the device side of PCIe.  Outputs and responses stay in host memory.
+    bool vram = false;
+    uint8_t *vmem = nullptr;
+    WorkerReq *v_req = nullptr;
+    uint32_t *v_mark = nullptr;                         // 16 words (64 B) per slot
+    std::vector<uint8_t *> v_img;
     std::vector<uint32_t> seq;                          // per slot: last request number posted
     std::atomic<uint64_t> free_mask{0};                 // bit i: slot i free
     std::atomic<bool> closed{false};                    // stopped: every later call is declined
@@ -439,6 +458,7 @@ struct Worker {
         if (stream) (void)hipStreamDestroy(stream);
         retire(h_slots, true);
         for (uint8_t *p : stage_h) retire(p, true);
+        retire(vmem, false);
         retire(d_state, false);
         retire(d_enc, false);
         retire(d_ver, false);
@@ -529,6 +549,8 @@ hipError_t worker_stream(int device, hipStream_t &out) {
 hipError_t launch(Worker &w, uint32_t g) {
     WorkerArgs a{};
     a.slots = w.d_slots;
+    a.vreq = w.vram ? w.v_req : nullptr;
+    a.vmark = w.vram ? w.v_mark : nullptr;
     for (int m = 0; m < 3; ++m) {
         a.pat[m] = w.views[m].pat;
         a.recs[m] = w.views[m].recs;
@@ -562,6 +584,11 @@ hipError_t launch(Worker &w, uint32_t g) {
         default: hipLaunchKernelGGL(gf_worker<4>, dim3(w.nslots), dim3(256), 0, w.stream, a); break;
     }
     return hipGetLastError();
+}
+
+hipError_t upload_zero(void *d, size_t bytes) {
+    std::vector<uint8_t> z(bytes, 0);
+    return upload(d, z.data(), bytes);
 }
 
 int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard, std::unique_ptr<Worker> &out) {
@@ -611,6 +638,24 @@ int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard
         HIP_TRY(hipHostGetDevicePointer((void **)&w->stage_d[i], w->stage_h[i], 0));
     }
     w->seq.assign(nslots, 0);
+    {
+        const char *tp = std::getenv("RSGPU_WORKER_TRANSPORT");
+        int large_bar = 0;
+        (void)hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ctx->device);
+        // the CPU writes fine-grained VRAM through its device pointer only
+        // when the whole VRAM is mapped through the BAR (large BAR)
+        if (tp && std::strcmp(tp, "vram") == 0 && large_bar) {
+            const size_t img = round_up(w->stage_cap, 256);
+            const size_t bytes = (size_t)nslots * (64 + 64 + img);
+            HIP_TRY(hipExtMallocWithFlags((void **)&w->vmem, bytes, hipDeviceMallocFinegrained));
+            w->v_req = (WorkerReq *)w->vmem;
+            w->v_mark = (uint32_t *)(w->vmem + (size_t)nslots * 64);
+            HIP_TRY(upload_zero(w->vmem, (size_t)nslots * 128));
+            w->v_img.resize(nslots);
+            for (int i = 0; i < nslots; ++i) w->v_img[i] = w->vmem + (size_t)nslots * 128 + (size_t)i * img;
+            w->vram = true;
+        }
+    }
     w->free_mask.store(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
     out = std::move(w);
     return RSGPU_OK;
@@ -628,10 +673,23 @@ int acquire_slot(Worker &w) {
 }
 void release_slot(Worker &w, int i) { w.free_mask.fetch_or(1ull << i, std::memory_order_release); }
 
-// every granule of slot s's request line: payload rq[g], tag `tag`
-void post_line(WorkerSlot &s, const uint32_t (&rq)[8], uint32_t tag) {
+// slot i's request line: pinned host memory, or VRAM through the BAR
+WorkerReq &req_line(Worker &w, int i) { return w.vram ? w.v_req[i] : w.h_slots[i].req; }
+// slot i's start mark (VRAM: read through the BAR, on the deadline path only)
+uint32_t start_mark(Worker &w, int i) {
+    return w.vram ? __atomic_load_n(&w.v_mark[(size_t)i * 16], __ATOMIC_ACQUIRE)
+                  : __atomic_load_n(&w.h_slots[i].resp.started, __ATOMIC_ACQUIRE);
+}
+
+// every granule of slot i's request line: payload rq[g], tag `tag`, each
+// one aligned 8-B store; the check word is rq[kWfSum]
+void post_line(Worker &w, int i, const uint32_t (&rq)[8], uint32_t tag) {
+    WorkerReq &r = req_line(w, i);
     for (int g = 0; g < 8; ++g)
-        __atomic_store_n(&s.req.g[g], (uint64_t)rq[g] | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
+        __atomic_store_n(&r.g[g], (uint64_t)rq[g] | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
+    // the BAR mapping is write-combining: flush the line now (a doorbell left
+    // in the WC buffer waited milliseconds in r03_mailbox_probe_vram_direct)
+    if (w.vram) __builtin_ia32_sfence();
 }
 
 // Posts request `rq` (payloads) on slot i and waits for its response;
@@ -660,9 +718,9 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
     using clk = std::chrono::steady_clock;
     WorkerSlot &s = w.h_slots[i];
     const uint32_t n = ++w.seq[i];
-    post_line(s, rq, n);
+    post_line(w, i, rq, n);
     auto retract = [&] {
-        post_line(s, rq, n - 1);
+        post_line(w, i, rq, n - 1);
         --w.seq[i];
     };
     auto fail = [&](int err) {
@@ -716,16 +774,15 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
         }
         if (now >= t_deadline) {
             cur = w.gen.load(std::memory_order_acquire);
-            if (__atomic_load_n(&s.resp.started, __ATOMIC_ACQUIRE) != cur) {
+            if (start_mark(w, i) != cur) {
                 retract();
                 std::atomic_thread_fence(std::memory_order_seq_cst);
-                if (__atomic_load_n(&s.resp.started, __ATOMIC_ACQUIRE) != cur &&
-                    (uint32_t)__atomic_load_n(&s.resp.done, __ATOMIC_ACQUIRE) != n) {
+                if (start_mark(w, i) != cur && (uint32_t)__atomic_load_n(&s.resp.done, __ATOMIC_ACQUIRE) != n) {
                     w.retracted.fetch_add(1, std::memory_order_relaxed);
                     return kWorkerDeclined;
                 }
                 ++w.seq[i];  // == n again
-                post_line(s, rq, n);
+                post_line(w, i, rq, n);
             }
             t_deadline = now + w.timeout;
         }
@@ -749,10 +806,9 @@ int quiesce(Worker &w) {
         // running (or its launch pending): a stop request on slot 0; its
         // workgroup raises `closing` and every other one leaves on its next
         // poll (the other mailboxes' request numbers stay as they are)
-        WorkerSlot &s = w.h_slots[0];
-        const uint32_t n = ++w.seq[0];
-        for (int g = 0; g < 8; ++g)
-            __atomic_store_n(&s.req.g[g], (uint64_t)(g == kWfOp ? 0xffu : 0u) | ((uint64_t)n << 32), __ATOMIC_RELEASE);
+        uint32_t rq[8] = {0xffu, 0, 0, 0, 0, 0, 0, 0};
+        rq[kWfSum] = worker_req_sum(rq);
+        post_line(w, 0, rq, ++w.seq[0]);
     }
     const hipError_t he = hipStreamSynchronize(w.stream);
     return he == hipSuccess ? RSGPU_OK : hip_fail(he, "worker stop");
@@ -852,16 +908,29 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
     for (int r = 1; r < n && split; ++r) split = rows[r] == rows[0] + (size_t)r * S;
     const uint8_t *img = split ? (const uint8_t *)host_device_ptr(rows[0], (size_t)(n - 1) * S + (S + 15) / 16 * 16)
                                : nullptr;
-    if (!img) {  // stage through the slot's image
-        img = w->stage_d[i];
+    const uint8_t *in = img, *out = img;
+    if (w->vram) {
+        // the rows it reads go to the slot's VRAM image (write-combined
+        // through the BAR); the fence orders them before the request line
+        // (posted writes to one device land in order)
+        uint8_t *vi = w->v_img[i];
+        for (int r = 0; r < n; ++r)
+            if ((rd >> r) & 1) std::memcpy(vi + (size_t)r * S, rows[r], S);
+        __builtin_ia32_sfence();
+        in = vi;
+        if (!out) out = w->stage_d[i];  // the written rows come back through host memory
+        if (op == kWopVerify || !wr) out = in;  // (nothing written)
+    } else if (!img) {  // stage through the slot's image
+        in = out = w->stage_d[i];
         for (int r = 0; r < n; ++r)
             if ((rd >> r) & 1) std::memcpy(w->stage_h[i] + (size_t)r * S, rows[r], S);
     }
-    uint32_t rq[8] = {op, (uint32_t)S, mask, (uint32_t)S, (uint32_t)(uintptr_t)img,
-                      (uint32_t)((uintptr_t)img >> 32), (uint32_t)(uintptr_t)img, (uint32_t)((uintptr_t)img >> 32)};
+    uint32_t rq[8] = {op, (uint32_t)S, mask, 0, (uint32_t)(uintptr_t)in, (uint32_t)((uintptr_t)in >> 32),
+                      (uint32_t)(uintptr_t)out, (uint32_t)((uintptr_t)out >> 32)};
+    rq[kWfSum] = worker_req_sum(rq);
     uint32_t status = 0;
     int e = post_and_wait(*w, i, rq, status);
-    if (e == RSGPU_OK && img == w->stage_d[i])
+    if (e == RSGPU_OK && out == w->stage_d[i])
         for (int r = 0; r < n; ++r)
             if ((wr >> r) & 1) std::memcpy(rows[r], w->stage_h[i] + (size_t)r * S, S);
     release_slot(*w, i);

@@ -52,8 +52,25 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(const PieceArgs a) {
         __builtin_amdgcn_make_buffer_rsrc((void *)(a.src + (size_t)r * a.src_pitch), (short)0, (int)a.src_span, 0x00020000);
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc((void *)(a.dst + (size_t)r * a.dst_pitch), (short)0, (int)a.dst_span, 0x00020000);
-    // past the last piece the range check returns zeros (never a fault)
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, o * a.src_stride + v * 16u, 0, 0);
+    const uint32_t voff = o * a.src_stride + v * 16u;
+    u32x4 x;
+    if (v == a.nvec - 1 && a.part && o == a.nobj - 1) {
+        // the launch's last piece ends inside its last 16-B vector, and the
+        // range check zeroes every dword that reaches past src_span: byte loads
+        x = u32x4{0u, 0u, 0u, 0u};
+        for (uint32_t b = 0; b < a.part; ++b) {
+            const uint32_t y = __builtin_amdgcn_raw_buffer_load_b8(rs, voff + b, 0, 0);
+            const uint32_t sh = 8u * (b & 3u);
+            if (b < 4) x[0] |= y << sh;
+            else if (b < 8) x[1] |= y << sh;
+            else if (b < 12) x[2] |= y << sh;
+            else x[3] |= y << sh;
+        }
+    } else {
+        // a piece's last vector may run into the next piece or gap: read,
+        // never written (store_row below writes shard_len bytes)
+        x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0);
+    }
     store_row<0>(x, rd, o * a.dst_stride + v * 16u, 0, v == a.nvec - 1 ? a.part : 0u);
 }
 
