@@ -164,16 +164,28 @@ int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
  * Results, checks and errors are exactly those of the stream path.
  *   nslots     mailboxes = resident workgroups (1..64; 0: 8)
  *   idle_us    the kernel leaves after this long without any request (0: 50 ms)
- *              and the next call relaunches it; while it runs, a
- *              hipDeviceSynchronize in the process waits for it to leave
+ *              and the next call relaunches it
  *   max_shard  the largest shard_len served (0: 4 KiB; the worker is ahead of the
  *              stream path up to ~40 KB objects and level with it at 64 KiB)
  * Calling it again restarts the worker with the new settings.  Multi-device
- * contexts: one worker per entry.  Requires data+parity <= 16
- * (RSGPU_ERR_NOT_IMPLEMENTED otherwise). */
+ * contexts: one worker per entry (a start that fails on one entry stops the
+ * others).  Requires data+parity <= 16 (RSGPU_ERR_NOT_IMPLEMENTED otherwise).
+ * Beside a resident kernel (DESIGN.md §5 "The worker beside the rest of the
+ * library"): it runs on a non-blocking stream of its own hardware queue, so
+ * other streams and the null stream never wait for it; the library defers its
+ * own device / pinned frees while a worker runs (hipFree and hipHostFree wait
+ * for every kernel of the device) and parks every worker around
+ * rsgpu_host_free / rsgpu_host_unregister; a caller's own hipDeviceSynchronize,
+ * hipFree or hipHostFree still waits until the worker idles out.  A request
+ * whose workgroup has not started within RSGPU_WORKER_TIMEOUT_US (200 ms) is
+ * taken back and the call takes the stream path.  On large-BAR devices the
+ * request lines and the input rows go through fine-grained VRAM the CPU
+ * writes through the BAR (RSGPU_WORKER_TRANSPORT=host keeps them in pinned
+ * host memory); outputs and responses are written to host memory. */
 int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard);
-/* Stops the worker (waits for calls in flight); the per-object calls go back
- * to the stream path.  rsgpu_destroy stops it too. */
+/* Stops the worker (waits for calls in flight; calls arriving meanwhile take
+ * the stream path); the per-object calls go back to the stream path.
+ * rsgpu_destroy stops it too. */
 int rsgpu_worker_stop(rsgpu_ctx *ctx);
 /* Calls the worker served, calls it declined because every mailbox was busy
  * (they took the stream path), and kernel launches so far (the first call
@@ -342,7 +354,9 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
 int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *present,
                        const size_t *shard_lens, int nobj, int *ok);
 
-/* Pinned host memory helpers (hipHostRegister / hipHostMalloc). */
+/* Pinned host memory helpers (hipHostRegister / hipHostMalloc).  free and
+ * unregister park any resident worker around the runtime call (it would
+ * otherwise wait for the worker to idle out). */
 int rsgpu_host_register(void *p, size_t len);
 int rsgpu_host_unregister(void *p);
 int rsgpu_host_alloc(size_t len, void **out);

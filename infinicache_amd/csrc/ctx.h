@@ -142,9 +142,18 @@ struct rsgpu_ctx {
     uint32_t *d_ctab = nullptr;      // [256][8] coefficient tables (gf_apply_lanes)
     std::mutex ctab_mu;              // guards the d_ctab upload (retried after a failure)
     rsgpu::StatusScratch scratch;    // multi-reporter status of the masked decode
-    // rsgpu_worker_start (null: off); read with std::atomic_load: a call in
-    // flight keeps the worker alive while a stop detaches it
+    // rsgpu_worker_start (null: off).  `worker` owns it (starts, stops,
+    // parks and stats; std::atomic_load / _store).  The per-object calls read
+    // `worker_raw` inside a reader epoch (WorkerRef, gf_worker.hip): a stop
+    // detaches the pointer, flips the epoch and waits for the readers counted
+    // in the old one before it drops its reference, so a call never touches a
+    // freed worker and no shared lock sits on the per-call path (the
+    // shared_ptr atomics of the first round-4 build took libstdc++'s mutex
+    // pool on every call: 16 callers' pairs/s halved, r04_lat_worker_1k_host.txt).
     std::shared_ptr<rsgpu::Worker> worker;
+    std::atomic<rsgpu::Worker *> worker_raw{nullptr};
+    std::atomic<uint32_t> worker_epoch{0};
+    std::atomic<int32_t> worker_readers[2] = {};
     std::mutex worker_mu;            // starts and stops
     // Multi-device context (rsgpu_create_multi / RSGPU_ALL_DEVICES): one
     // single-device context per entry of the device list.  Per-object calls

@@ -422,11 +422,14 @@ struct Worker {
     WorkerSlot *h_slots = nullptr, *d_slots = nullptr;  // coherent pinned mailboxes
     std::vector<uint8_t *> stage_h, stage_d;            // per slot: a coherent pinned object image
     size_t stage_cap = 0;
-    // VRAM transport (RSGPU_WORKER_TRANSPORT=vram): request lines, start
-    // marks and per-slot input images in one fine-grained VRAM allocation the
-    // CPU writes through the BAR (same address on both sides); the input
-    // rows are copied there, so the kernel's poll and its row loads stay on
-    // the device side of PCIe.  Outputs and responses stay in host memory.
+    // VRAM transport (the default on large-BAR devices; RSGPU_WORKER_TRANSPORT
+    // =host keeps round 3's): request lines, start marks and per-slot input
+    // images in one fine-grained VRAM allocation the CPU writes through the
+    // BAR (same address on both sides); the input rows are copied there, so
+    // the kernel's poll and its row loads stay on the device side of PCIe.
+    // Outputs and responses stay in host memory.  1 KiB objects: fused
+    // encode+verify 8.4 -> 6.9 us p50, decode 7.3 -> 5.7 us
+    // (profiles/r04_lat_worker_1k_{host,vram}.txt, same box).
     bool vram = false;
     uint8_t *vmem = nullptr;
     WorkerReq *v_req = nullptr;
@@ -644,7 +647,7 @@ int worker_create(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_shard
         (void)hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ctx->device);
         // the CPU writes fine-grained VRAM through its device pointer only
         // when the whole VRAM is mapped through the BAR (large BAR)
-        if (tp && std::strcmp(tp, "vram") == 0 && large_bar) {
+        if (!(tp && std::strcmp(tp, "host") == 0) && large_bar) {
             const size_t img = round_up(w->stage_cap, 256);
             const size_t bytes = (size_t)nslots * (64 + 64 + img);
             HIP_TRY(hipExtMallocWithFlags((void **)&w->vmem, bytes, hipDeviceMallocFinegrained));
@@ -857,18 +860,45 @@ void track_worker(rsgpu_ctx *ctx, bool on) {
     else g_live.erase(ctx);
 }
 
+// A reader epoch on ctx's worker (rsgpu_ctx::worker_raw): counted in the
+// parity of the epoch current when the pointer is read (the epoch is read
+// again after counting: a reader counted in a parity that flipped meanwhile
+// tries again), so stop_locked's wait covers every reader that can hold it.
+struct WorkerRef {
+    rsgpu_ctx *c;
+    uint32_t p;
+    Worker *w;
+    explicit WorkerRef(rsgpu_ctx *ctx) : c(ctx) {
+        for (;;) {
+            const uint32_t e = c->worker_epoch.load(std::memory_order_seq_cst);
+            p = e & 1u;
+            c->worker_readers[p].fetch_add(1, std::memory_order_seq_cst);
+            if (c->worker_epoch.load(std::memory_order_seq_cst) == e) break;
+            c->worker_readers[p].fetch_sub(1, std::memory_order_seq_cst);
+        }
+        w = c->worker_raw.load(std::memory_order_seq_cst);
+    }
+    ~WorkerRef() { c->worker_readers[p].fetch_sub(1, std::memory_order_release); }
+    WorkerRef(const WorkerRef &) = delete;
+    WorkerRef &operator=(const WorkerRef &) = delete;
+};
+
 // ctx's worker stopped and detached (ctx->worker_mu and g_park_mu held)
 int stop_locked(rsgpu_ctx *ctx) {
     std::shared_ptr<Worker> w = std::atomic_exchange(&ctx->worker, std::shared_ptr<Worker>());
     track_worker(ctx, false);
     if (!w) return RSGPU_OK;
+    // no new call finds it; the calls that may hold it finish (they are
+    // declined below, or finish a request they already posted)
+    ctx->worker_raw.store(nullptr, std::memory_order_seq_cst);
+    const uint32_t old = ctx->worker_epoch.fetch_add(1, std::memory_order_seq_cst) & 1u;
     w->closed.store(true, std::memory_order_release);
     DeviceGuard dg_;
     int e = ctx->use_device(dg_, false);
     if (!e) e = quiesce(*w);
+    while (ctx->worker_readers[old].load(std::memory_order_acquire) != 0) std::this_thread::yield();
     if (w->trace) print_trace(*w);
     // its kernel has left: what was retired while it ran may be freed now
-    // (calls still holding `w` are declined; the last reference frees it)
     worker_count(-1);
     return e;
 }
@@ -878,10 +908,10 @@ int stop_locked(rsgpu_ctx *ctx) {
 // The worker serves one object when it can: returns RSGPU_OK with *bad set
 // (0 / 1), kWorkerDeclined to use the stream path, or an error.
 int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *const *rows, uint32_t *bad) {
-    // a reference: a concurrent rsgpu_worker_stop detaches the worker, and
-    // its memory lives until this call is done with it
-    const std::shared_ptr<Worker> ref = std::atomic_load(&ctx->worker);
-    Worker *w = ref.get();
+    // a reader epoch: a concurrent rsgpu_worker_stop detaches the worker and
+    // frees it only after this call is done with it
+    const WorkerRef ref(ctx);
+    Worker *w = ref.w;
     if (!w || S > w->max_shard || S == 0) return kWorkerDeclined;
     const int n = ctx->n, k = ctx->k;
     const uint32_t full = (1u << n) - 1;
@@ -1001,7 +1031,9 @@ int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_
     std::unique_ptr<Worker> w;
     if ((e = worker_create(ctx, nslots, idle_us, max_shard, w))) return e;
     worker_count(+1);  // before its first launch (the first request's)
-    std::atomic_store(&ctx->worker, std::shared_ptr<Worker>(w.release()));
+    std::shared_ptr<Worker> sp(w.release());
+    ctx->worker_raw.store(sp.get(), std::memory_order_seq_cst);
+    std::atomic_store(&ctx->worker, std::move(sp));
     track_worker(ctx, true);
     return RSGPU_OK;
 }

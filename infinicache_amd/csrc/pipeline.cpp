@@ -170,8 +170,15 @@ int rsgpu_host_alloc(size_t len, void **out) {
     *out = nullptr;
     if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
     // 64 B of slack past the caller's length: kernels may read a Split buffer
-    // in place, and a row's last 16-B vector can run past the buffer's end
-    HIP_TRY(hipHostMalloc(out, len + 64, hipHostMallocDefault));
+    // in place, and a row's last 16-B vector can run past the buffer's end.
+    // Flags: RSGPU_HOST_ALLOC=coherent takes the worker's own kind
+    // (Mapped | Coherent) for a measurement
+    static const unsigned flags = [] {
+        const char *e = std::getenv("RSGPU_HOST_ALLOC");
+        return e && std::strcmp(e, "coherent") == 0 ? (unsigned)(hipHostMallocMapped | hipHostMallocCoherent)
+                                                    : (unsigned)hipHostMallocDefault;
+    }();
+    HIP_TRY(hipHostMalloc(out, len + 64, flags));
     pin_add(*out, len, len + 64);
     return RSGPU_OK;
 }

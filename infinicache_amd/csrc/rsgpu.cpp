@@ -824,7 +824,7 @@ static int reconstruct_common(rsgpu_ctx *ctx, uint8_t *const *shards, const size
         if (!shards[plan->out_rows[r]]) return RSGPU_ERR_INVALID_ARG;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
-    if (std::atomic_load(&ctx->worker)) {
+    if (ctx->worker_raw.load(std::memory_order_relaxed)) {
         // the worker writes every missing row it rebuilds through rows[i]:
         // each needs a buffer (ReconstructData: the missing data rows only)
         bool bufs = true;

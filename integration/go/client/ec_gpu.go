@@ -149,37 +149,58 @@ func newGPUEncoder(dataShards, parityShards int) (reedsolomon.Encoder, error) {
 
 // ---- helpers ---------------------------------------------------------------
 
-// stagePool keeps C-owned pinned images (rsgpu_host_alloc) by size.  Go copies
-// shard bytes into them (C memory holding no pointers); the kernels access
-// them in place.
+// stagePool keeps C-owned pinned images (rsgpu_host_alloc) in power-of-two
+// size classes (a request of size bytes gets an image of at least size; the
+// caller uses its first size bytes, and rsgpu_host_alloc's 64 B of slack lie
+// past the class).  Go copies shard bytes into them (C memory holding no
+// pointers); the kernels access them in place.  At most 8 images per class
+// and stagePoolCap bytes in all are kept: config 5 mixes 4 KiB-100 MiB
+// objects, and an exact-size pool kept one set per distinct size.  Each
+// rsgpu_host_free parks a resident worker for its duration (rsgpu.h), so the
+// pool frees rarely.
 type stagePool struct {
-	mu   sync.Mutex
-	free map[int][]unsafe.Pointer
+	mu    sync.Mutex
+	free  map[int][]unsafe.Pointer
+	bytes int
+}
+
+const stagePoolCap = 512 << 20
+
+func stageClass(size int) int {
+	c := 4096
+	for c < size {
+		c <<= 1
+	}
+	return c
 }
 
 func (p *stagePool) get(size int) (unsafe.Pointer, error) {
+	cls := stageClass(size)
 	p.mu.Lock()
-	if l := p.free[size]; len(l) > 0 {
+	if l := p.free[cls]; len(l) > 0 {
 		ptr := l[len(l)-1]
-		p.free[size] = l[:len(l)-1]
+		p.free[cls] = l[:len(l)-1]
+		p.bytes -= cls
 		p.mu.Unlock()
 		return ptr, nil
 	}
 	p.mu.Unlock()
 	var ptr unsafe.Pointer
-	if rc := C.rsgpu_host_alloc(C.size_t(size), &ptr); rc != 0 {
+	if rc := C.rsgpu_host_alloc(C.size_t(cls), &ptr); rc != 0 {
 		return nil, rsErr(rc)
 	}
 	return ptr, nil
 }
 
 func (p *stagePool) put(size int, ptr unsafe.Pointer) {
+	cls := stageClass(size)
 	p.mu.Lock()
 	if p.free == nil {
 		p.free = map[int][]unsafe.Pointer{}
 	}
-	if len(p.free[size]) < 8 {
-		p.free[size] = append(p.free[size], ptr)
+	if len(p.free[cls]) < 8 && p.bytes+cls <= stagePoolCap {
+		p.free[cls] = append(p.free[cls], ptr)
+		p.bytes += cls
 		ptr = nil
 	}
 	p.mu.Unlock()
@@ -197,6 +218,7 @@ func (p *stagePool) drain() {
 		}
 	}
 	p.free = nil
+	p.bytes = 0
 }
 
 // cbytes is a Go view of n bytes of C memory (Go 1.12: no unsafe.Slice).
