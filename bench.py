@@ -77,11 +77,13 @@ WORKLOADS = {
                              desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, shard-major "
                                   "(16-B aligned pieces), per-object random erasure pair (device-resident "
                                   "present masks)"),
+    # the mixed 1 KiB shape as the library lays it out (rsgpu_shardmajor_layout:
+    # whole 128-B line pieces for S = 103)
     "small1k_sm_mixed_a128": dict(k=10, p=2, nbytes=1 << 10, batch=1 << 20, lost=(0, 5), ops=("encode", "decode"),
-                                  shard_major=True, oalign=128, mixed=True,
+                                  shard_major=True, oalign="library", mixed=True,
                                   desc="RS(10+2) encode+decode, 1 KiB objects, batch 1048576/GPU, shard-major "
-                                       "(128-B aligned pieces: one line each), per-object random erasure pair "
-                                       "(device-resident present masks)"),
+                                       "in rsgpu_shardmajor_layout's geometry (128-B pieces: one line each), "
+                                       "per-object random erasure pair (device-resident present masks)"),
     "small_sm": dict(k=10, p=2, nbytes=4 << 10, batch=256 << 10, lost=(0, 5), ops=("encode", "decode"),
                      shard_major=True, oalign=1,
                      desc="RS(10+2) encode+decode, 4 KiB objects, batch 262144/GPU, shard-major"),
@@ -646,9 +648,12 @@ def main():
         nobj = shard_objects(nobj, rank, world)[1]
     S = (w["nbytes"] + k - 1) // k
     if w.get("shard_major"):  # [shard][object]: object o's piece of shard i at i*pitch + o*stride
-        oal = w.get("oalign", 1)
-        stride = (S + oal - 1) // oal * oal
-        pitch = (nobj * stride + 255) // 256 * 256
+        if w.get("oalign") == "library":  # the geometry rsgpu_shardmajor_layout chooses
+            stride, pitch = ia.shardmajor_layout(S, nobj)
+        else:
+            oal = w.get("oalign", 1)
+            stride = (S + oal - 1) // oal * oal
+            pitch = (nobj * stride + 255) // 256 * 256
     else:                     # [object][shard][pitch]
         pal = w.get("palign", 256)
         pitch = (S + pal - 1) // pal * pal

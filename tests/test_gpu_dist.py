@@ -142,5 +142,5 @@ def test_bench_two_ranks_shared_gpu(gpu, tmp_path):
     # next #3): the driver's N = 2/4/8 lines carry it too
     cpu = out["cpu_baseline"]
     assert cpu is not None and cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
-    assert "bit-exact vs GPU: True" in cpu["sample"], cpu["sample"]
+    assert "bit-exact vs GPU" in cpu["sample"] and cpu["sample"].endswith(": True"), cpu["sample"]
     assert out["roofline"]["traffic_source"].startswith(("committed profile", "none"))
