@@ -89,7 +89,9 @@ int rsgpu_shardmajor_layout(size_t shard_len, int nobj, size_t *obj_stride, size
     const size_t s128 = round_up(shard_len, 128), s16 = round_up(shard_len, 16);
     const size_t stride = (s128 - shard_len) * 4 <= shard_len ? s128 : s16;
     const size_t p = round_up(std::max<size_t>(1, (size_t)nobj) * stride, 256);
-    if (p >= ((size_t)1 << 32) / 64) return RSGPU_ERR_INVALID_ARG;  // (data+parity)*pitch < 4 GiB for <= 64 shards
+    // the coding calls require (data+parity) * pitch < 4 GiB (they check it);
+    // here only a pitch no code of >= 2 shards can use is refused
+    if (p >= ((size_t)1 << 31)) return RSGPU_ERR_INVALID_ARG;
     *obj_stride = stride;
     *pitch = p;
     return RSGPU_OK;

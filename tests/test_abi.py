@@ -224,3 +224,32 @@ def test_dev_objs_argument_checks():
         enc.decode_dev_objs([(0x1000, 100, 112)], [0, 0, 0] + [1] * 9, 0x2000)
     with pytest.raises(ia.InvalidArgument):
         enc.decode_dev_objs([(0x1000, 100, 112)], [1] * 12, 0)  # no flag array
+
+
+@pytest.mark.parametrize("S,nobj,stride", [(103, 1 << 20, 128), (100, 10, 112), (1, 5, 16), (410, 3, 512),
+                                            (4096, 7, 4096), (4099, 2, 4224), (128, 1, 128), (17, 9, 32)])
+def test_shardmajor_layout(S, nobj, stride):
+    """rsgpu_shardmajor_layout (no device): whole 128-B lines when the gap is
+    at most S/4 (the encode still codes the batch as one object), else 16-B
+    aligned pieces; the pitch holds every piece, rounded up to 256."""
+    st, pitch = ia.shardmajor_layout(S, nobj)
+    assert st == stride
+    assert pitch % 256 == 0 and pitch >= nobj * st and pitch - nobj * st < 256
+    with pytest.raises(ia.ErrShardNoData):
+        ia.shardmajor_layout(0, 4)
+
+
+def test_copy_pieces_argument_checks():
+    """rsgpu_copy_pieces validates before any device work: rows beyond the
+    code, overlapping pieces (a stride below shard_len), zero shard_len;
+    then fails loudly without a device."""
+    enc = ia.New(10, 2)
+    with pytest.raises(ia.InvalidArgument):
+        enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 128, 100, 4, rows=[12])
+    with pytest.raises(ia.InvalidArgument):
+        enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 64, 100, 4)
+    with pytest.raises(ia.ErrShardNoData):
+        enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 128, 0, 4)
+    if not ia.device_ok(0):
+        with pytest.raises(ia.NoDevice):
+            enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 128, 100, 4)

@@ -239,3 +239,36 @@ def test_worker_multi_entry_context(gpu):
             assert np.array_equal(got[j], full[j])
     assert enc.worker_stats()["served"] >= 6
     assert all(c > b for c, b in zip(enc.device_calls(), base)), (enc.device_calls(), base)
+
+
+def test_worker_deadline_takes_request_back(gpu, monkeypatch):
+    """post_and_wait's deadline (RSGPU_WORKER_TIMEOUT_US, read when the worker
+    starts): with a 1 us deadline, a call that had to relaunch the idle
+    kernel finds no start mark on its slot in time, takes its request back
+    and goes down the stream path (declined); a call whose workgroup is
+    running waits for it.  Every result is exact either way, and every call
+    is either served or declined."""
+    k, p = 10, 2
+    n = k + p
+    monkeypatch.setenv("RSGPU_WORKER_TIMEOUT_US", "1")
+    enc = ia.New(k, p)
+    enc.worker_start(nslots=2, idle_us=1000)  # leaves after 1 ms without requests
+    calls = 0
+    for i in range(40):
+        S = 103 + 7 * i
+        full = _full(k, p, S, 400 + i)
+        sh = [full[j].copy() if j < k else np.zeros(S, np.uint8) for j in range(n)]
+        assert enc.EncodeVerify(sh)
+        for j in range(n):
+            assert np.array_equal(sh[j], full[j]), (i, j)
+        got = [None if j in (i % n, (i + 4) % n) else sh[j] for j in range(n)]
+        assert enc.DecodeVerify(got)
+        for j in range(n):
+            assert np.array_equal(got[j], full[j]), (i, j)
+        calls += 2
+        if i % 2:
+            time.sleep(0.005)  # the kernel idles out: the next call relaunches it
+    st = enc.worker_stats()
+    assert st["served"] + st["declined"] == calls, st
+    assert st["declined"] > 0 and st["launches"] >= 2, st
+    enc.worker_stop()

@@ -43,6 +43,13 @@ for s in $STEPS; do
               run pmc_fetch_$wl 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --workload $wl
               run pmc_write_$wl 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$wl -o run --output-format csv -- python3 bench.py --no-cpu --steps 5 --workload $wl
             done ;;
+    worker) run pytest_worker 600 python -u -m pytest tests/test_gpu_worker.py tests/test_gpu_worker_concurrency.py -m gpu -x -v -s --timeout 150 --timeout-method thread ;;
+    lat_sizes) for b in ${LAT_SIZES:-1024 4096 16384 40960}; do
+              LAT_WORKER=16 LAT_BYTES=$b run lat_worker_vram_$b 120 ./tools/lat_bench 200 1
+              RSGPU_WORKER_TRANSPORT=host LAT_WORKER=16 LAT_BYTES=$b run lat_worker_host_$b 120 ./tools/lat_bench 200 1
+            done ;;
+    lat_alloc) LAT_BYTES=1048576 run lat_stream_1m_default 120 ./tools/lat_bench 200 1
+            RSGPU_HOST_ALLOC=coherent LAT_BYTES=1048576 run lat_stream_1m_coherent 120 ./tools/lat_bench 200 1 ;;
     avail)  run avail 120 rocprofv3 --list-avail ;;
     pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
