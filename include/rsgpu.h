@@ -105,7 +105,10 @@ int rsgpu_device_ok(int device);
 
 /* ---- per-object host-memory API (what the Go shim forwards to) ---------- */
 /* shards[i]: caller-owned host buffer of lens[i] bytes; lens[i] == 0 marks a
- * nil/empty shard.  nshards must equal data+parity (else TOO_FEW_SHARDS). */
+ * nil/empty shard.  nshards must equal data+parity (else TOO_FEW_SHARDS).
+ * Shards of any length, as upstream: an object whose staged rows would pass
+ * 1 GiB is coded in column slabs (each byte column is independent), so the
+ * 4 GiB a device pass addresses is no limit here. */
 
 /* Encode (upstream Encode; ecRedis.go:390): checkShards(nilok=false), then
  * shards[k..k+p) = parity.  All shards must be allocated (len == size). */
@@ -340,7 +343,9 @@ int rsgpu_decode_dev_objs(rsgpu_ctx *ctx, const rsgpu_dev_obj *objs, int nobj, c
  * objects through the GPU over a ring of device slots / HIP streams so the
  * copies of one object overlap the kernel of another; they return when every
  * output is in host memory.  Host buffers should be pinned
- * (rsgpu_host_register / rsgpu_host_alloc) for the copies to run async. */
+ * (rsgpu_host_register / rsgpu_host_alloc) for the copies to run async.
+ * Objects whose data+parity rows pass 1 GiB go through the per-object path
+ * above (column slabs) in the same call. */
 
 /* objs[o]: the Split() backing array of object o — data+parity rows of
  * shard_lens[o] bytes each, contiguous (pitch = shard length).  Parity rows

@@ -43,6 +43,15 @@ struct Slot {
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Staged image bytes (rows x shard length) above which the host calls code
+// one object in column slabs (rsgpu.cpp run_host; the batch pipelines hand
+// such objects to it).  RSGPU_SLAB_BYTES overrides it, for tests.
+inline size_t slab_bytes() {
+    const char *v = std::getenv("RSGPU_SLAB_BYTES");
+    const long long b = v ? std::atoll(v) : 0;
+    return b >= 4096 ? (size_t)b : ((size_t)1 << 30);
+}
+
 inline bool debug_on() {
     static const bool on = std::getenv("RSGPU_DEBUG") != nullptr;
     return on;

@@ -237,23 +237,35 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
         });
     }
     const int k = ctx->k, p = ctx->p, n = ctx->n;
+    // objects past the slab size go through the per-object host path (coded
+    // in column slabs, rsgpu.cpp run_host), the rest through the pipeline
+    const size_t lim = slab_bytes();
+    std::vector<int> piped, big;
     size_t maxbytes = 0;
     for (int o = 0; o < nobj; ++o) {
         if (!objs[o]) return RSGPU_ERR_INVALID_ARG;
         if (shard_lens[o] == 0) return RSGPU_ERR_SHARD_NO_DATA;
-        if ((size_t)n * shard_lens[o] >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
+        if ((size_t)n * shard_lens[o] + 16 > lim) {
+            big.push_back(o);
+            continue;
+        }
+        piped.push_back(o);
         maxbytes = std::max(maxbytes, (size_t)n * shard_lens[o] + 16);
     }
     if (nobj == 0) return RSGPU_OK;
     DeviceGuard dg_;
     int e = ctx->use_device(dg_);
     if (e) return e;
+    for (int o : big)
+        if ((e = rsgpu_encode_image(ctx, objs[o], shard_lens[o], n))) return e;
+    if (piped.empty()) return RSGPU_OK;
     auto plan = ctx->plan_encode();
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
     if ((e = ensure_slots(ctx, maxbytes))) return e;
     hipError_t he = hipSuccess;
-    for (int o = 0; o < nobj && he == hipSuccess; ++o) {
-        PipeSlot &s = *ctx->pipe.slots[o % pipe_slots()];
+    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++q) {
+        const int o = piped[q];
+        PipeSlot &s = *ctx->pipe.slots[q % pipe_slots()];
         const size_t S = shard_lens[o];
         he = hipMemcpyAsync(s.d, objs[o], (size_t)k * S, hipMemcpyHostToDevice, s.stream);
         Layout L{s.d, 0, S, S, 1};
@@ -298,6 +310,8 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
             return e;
         });
     }
+    const size_t lim = slab_bytes();  // larger objects: per-object host path (encode_batch)
+    std::vector<int> piped, big;
     size_t maxbytes = 0;
     std::vector<std::shared_ptr<Plan>> plans(nobj);
     for (int o = 0; o < nobj; ++o) {
@@ -311,19 +325,30 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
         int e = np == n ? (plans[o] = ctx->plan_verify(), RSGPU_OK)
                         : ctx->plan_reconstruct(pr, false, true, plans[o]);
         if (e) return e;
-        if ((size_t)n * shard_lens[o] >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
+        if ((size_t)n * shard_lens[o] + 16 > lim) {
+            big.push_back(o);
+            continue;
+        }
+        piped.push_back(o);
         maxbytes = std::max(maxbytes, (size_t)n * shard_lens[o] + 16);
     }
     if (nobj == 0) return RSGPU_OK;
     DeviceGuard dg_;
     int e = ctx->use_device(dg_);
     if (e) return e;
+    for (int o : big) {
+        std::vector<size_t> lens(n);
+        for (int i = 0; i < n; ++i) lens[i] = present[(size_t)o * n + i] ? shard_lens[o] : 0;
+        if ((e = rsgpu_decode(ctx, shards + (size_t)o * n, lens.data(), n, &ok[o]))) return e;
+    }
+    if (piped.empty()) return RSGPU_OK;
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
     if ((e = ensure_slots(ctx, maxbytes))) return e;
     if ((e = ensure_flags(ctx, nobj))) return e;
     hipError_t he = hipSuccess;
-    for (int o = 0; o < nobj && he == hipSuccess; ++o) {
-        PipeSlot &s = *ctx->pipe.slots[o % pipe_slots()];
+    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++q) {
+        const int o = piped[q];
+        PipeSlot &s = *ctx->pipe.slots[q % pipe_slots()];
         Plan &plan = *plans[o];
         uint8_t *const *row = shards + (size_t)o * n;
         const size_t S = shard_lens[o], P = S;  // packed rows
@@ -358,7 +383,7 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
     e = drain(ctx);
     if (he != hipSuccess) return hip_fail(he, "rsgpu_decode_batch");
     if (e) return e;
-    for (int o = 0; o < nobj; ++o) ok[o] = ctx->pipe.h_bad[o] == 0;
+    for (int o : piped) ok[o] = ctx->pipe.h_bad[o] == 0;
     return RSGPU_OK;
 }
 

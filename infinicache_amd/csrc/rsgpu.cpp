@@ -157,9 +157,9 @@ namespace {
 //   * `then` (optional): a second plan run on the same device image after the
 //     first one's rows went back, whose check flag lands in *then_bad
 //     (Client.encode's Verify right after Encode: no second upload).
-int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
-             const std::vector<const uint8_t *> &in_src, const std::vector<uint8_t *> &out_dst,
-             uint32_t *bad, Plan *then = nullptr, uint32_t *then_bad = nullptr) {
+int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
+                  const std::vector<const uint8_t *> &in_src, const std::vector<uint8_t *> &out_dst,
+                  uint32_t *bad, Plan *then, uint32_t *then_bad) {
     if (then && (plan.nw < plan.R || then->nw != 0)) return RSGPU_ERR_INVALID_ARG;  // see `then` above
     // row offsets are 32-bit inside the pass (Pass::in_off / out_off)
     if ((size_t)nrows_staged * size + 16 >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
@@ -290,6 +290,40 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     if (bad) *bad = plan.nw < plan.R ? *s->h_bad : 0;
     if (then_bad) *then_bad = *s->h_bad;
     ctx->put_slot(std::move(s));
+    return RSGPU_OK;
+}
+
+// run_host_once for objects of any size.  Every operation is a byte-column
+// map (output byte b of a row depends on byte b of the input rows only), so
+// an object whose staged image would pass slab_bytes() — or the 4 GiB a
+// pass can address — is coded as consecutive column slabs [b0, b0 + L) of
+// every row, each one run_host_once on the rows' pointers offset by b0.
+// Upstream codes shards of any length (reedsolomon.Encoder has no size
+// limit); the slabs also bound the staging slot a huge object takes.  Check
+// flags are OR-ed over the slabs (Verify fails if any column mismatches).
+int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
+             const std::vector<const uint8_t *> &in_src, const std::vector<uint8_t *> &out_dst,
+             uint32_t *bad, Plan *then = nullptr, uint32_t *then_bad = nullptr) {
+    const size_t lim = slab_bytes();
+    if ((size_t)nrows_staged * size + 16 <= lim)
+        return run_host_once(ctx, plan, nrows_staged, size, in_src, out_dst, bad, then, then_bad);
+    const size_t L = std::max<size_t>(4096, ((lim - 16) / (size_t)nrows_staged) & ~(size_t)4095);
+    std::vector<const uint8_t *> in(in_src.size());
+    std::vector<uint8_t *> out(out_dst.size());
+    uint32_t bad_all = 0, then_all = 0;
+    for (size_t b0 = 0; b0 < size; b0 += L) {
+        const size_t l = std::min(L, size - b0);
+        for (size_t i = 0; i < in.size(); ++i) in[i] = in_src[i] + b0;
+        for (size_t i = 0; i < out.size(); ++i) out[i] = out_dst[i] + b0;
+        uint32_t b = 0, tb = 0;
+        const int e = run_host_once(ctx, plan, nrows_staged, l, in, out, bad ? &b : nullptr, then,
+                                    then_bad ? &tb : nullptr);
+        if (e) return e;
+        bad_all |= b;
+        then_all |= tb;
+    }
+    if (bad) *bad = bad_all;
+    if (then_bad) *then_bad = then_all;
     return RSGPU_OK;
 }
 
