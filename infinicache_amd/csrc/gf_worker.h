@@ -30,10 +30,14 @@ enum WorkerOp : uint32_t {
     kWopDecode = 5,        // fused Client.decode (atlas mode kAtlasDecode)
 };
 
-// granule payloads of a request line (rows at pitch = shard length: Split's
-// layout; kWfSum checks the other seven payloads)
-enum WorkerField { kWfOp = 0, kWfShardLen = 1, kWfMask = 2, kWfSum = 3, kWfInLo = 4, kWfInHi = 5, kWfOutLo = 6,
+// granule payloads of a request line; kWfSum checks the other seven.
+//   kWfOp:       operation (bits 0-7) | present mask << 8 (n <= 16 shards)
+//   kWfShardLen: bytes coded per row
+//   kWfPitch:    bytes between rows (Split's layout: the shard length; a
+//                column slice of a larger object: that object's shard length)
+enum WorkerField { kWfOp = 0, kWfShardLen = 1, kWfPitch = 2, kWfSum = 3, kWfInLo = 4, kWfInHi = 5, kWfOutLo = 6,
                    kWfOutHi = 7 };
+__host__ __device__ inline uint32_t worker_opmask(uint32_t op, uint32_t mask) { return (op & 0xffu) | (mask << 8); }
 
 // The request line's check word.  Every granule is one aligned 8-B store,
 // which the worker accepts only once its tag is current; the check word
@@ -44,7 +48,7 @@ enum WorkerField { kWfOp = 0, kWfShardLen = 1, kWfMask = 2, kWfSum = 3, kWfInLo 
 __host__ __device__ inline uint32_t worker_req_sum(const uint32_t *p) {
     auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
     uint32_t h = 0x5bd1e995u ^ (p[kWfOp] * 0x9E3779B1u);
-    h ^= rotl(p[kWfShardLen], 7) ^ rotl(p[kWfMask], 13) ^ p[kWfInLo] ^ rotl(p[kWfInHi], 3);
+    h ^= rotl(p[kWfShardLen], 7) ^ rotl(p[kWfPitch], 13) ^ p[kWfInLo] ^ rotl(p[kWfInHi], 3);
     h ^= rotl(p[kWfOutLo], 17) ^ rotl(p[kWfOutHi], 23);
     return h * 0x85EBCA6Bu ^ (h >> 15);
 }

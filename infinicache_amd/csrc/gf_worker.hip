@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
         }
         __syncthreads();
         const uint32_t found = rfl(sfound);
-        const uint32_t op = rfl(sreq[kWfOp]);
+        const uint32_t op = rfl(sreq[kWfOp]) & 0xffu;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         if (found != want || op > kWopDecode) {
             // idle (or a stop request): tell the host this slot's workgroup is gone
@@ -173,7 +173,10 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
             }
             return;
         }
-        const uint32_t S = rfl(sreq[kWfShardLen]), mask = rfl(sreq[kWfMask]) & a.nmask, pitch = S;
+        // S bytes of each row at `pitch` apart: a whole Split image (pitch ==
+        // S) or one column slice of a larger object (worker_run_split)
+        const uint32_t S = rfl(sreq[kWfShardLen]), mask = (rfl(sreq[kWfOp]) >> 8) & a.nmask;
+        const uint32_t pitch = rfl(sreq[kWfPitch]) ? rfl(sreq[kWfPitch]) : S;
         const uint64_t inb = (uint64_t)rfl(sreq[kWfInLo]) | ((uint64_t)rfl(sreq[kWfInHi]) << 32);
         const uint64_t outb = (uint64_t)rfl(sreq[kWfOutLo]) | ((uint64_t)rfl(sreq[kWfOutHi]) << 32);
         __syncthreads();  // sreq is rewritten by the next poll
@@ -197,7 +200,9 @@ __global__ __launch_bounds__(256) void gf_worker(const WorkerArgs a) {
         }
         const uint32_t kact = (uint32_t)__builtin_popcount(rows);
         const uint32_t nvec = (S + 15) / 16, tail = S - (nvec - 1) * 16;
-        const uint32_t wlast = pitch - (nvec - 1) * 16, part = wlast < 16 ? wlast : 0u;
+        // the last vector's bytes past S are not written: the next row's
+        // (pitch == S), or the next column slice's (another workgroup's)
+        const uint32_t part = tail < 16 ? tail : 0u;
         const uint32_t span = (a.n - 1) * pitch + nvec * 16;
         const __amdgpu_buffer_rsrc_t rsi = __builtin_amdgcn_make_buffer_rsrc((void *)inb, (short)0, (int)span, 0x00020000);
         const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc((void *)outb, (short)0, (int)span, 0x00020000);
@@ -717,11 +722,15 @@ void post_line(Worker &w, int i, const uint32_t (&rq)[8], uint32_t tag) {
 // way) and waited for.  A request whose workgroup is running is never taken
 // back — it would write into buffers the caller may have freed — and is
 // answered in microseconds; a kernel that dies is caught by hipStreamQuery.
-int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
-    using clk = std::chrono::steady_clock;
-    WorkerSlot &s = w.h_slots[i];
+uint32_t post(Worker &w, int i, const uint32_t (&rq)[8]) {
     const uint32_t n = ++w.seq[i];
     post_line(w, i, rq, n);
+    return n;
+}
+
+int wait_for(Worker &w, int i, const uint32_t (&rq)[8], const uint32_t n, uint32_t &status) {
+    using clk = std::chrono::steady_clock;
+    WorkerSlot &s = w.h_slots[i];
     auto retract = [&] {
         post_line(w, i, rq, n - 1);
         --w.seq[i];
@@ -738,8 +747,8 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
         const uint64_t d = __atomic_load_n(&s.resp.done, __ATOMIC_ACQUIRE);
         if ((uint32_t)d == n) {
             status = (uint32_t)(d >> 32);
-            if (w.trace && rq[kWfOp] < 6) {
-                auto &tr = w.tr[rq[kWfOp]];
+            if (w.trace && (rq[kWfOp] & 0xffu) < 6) {
+                auto &tr = w.tr[rq[kWfOp] & 0xffu];
                 tr[0].fetch_add(1);
                 for (int j = 0; j < 5; ++j) tr[1 + j].fetch_add(s.resp.pad[j]);
                 tr[6].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t_post).count());
@@ -790,6 +799,10 @@ int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
             t_deadline = now + w.timeout;
         }
     }
+}
+
+int post_and_wait(Worker &w, int i, const uint32_t (&rq)[8], uint32_t &status) {
+    return wait_for(w, i, rq, post(w, i, rq), status);
 }
 
 // Takes every mailbox (calls in flight finish first; w.closed / w.parked
@@ -905,6 +918,73 @@ int stop_locked(rsgpu_ctx *ctx) {
 
 }  // namespace
 
+// Objects past max_shard, up to kSplitMaxShard per shard, when their rows
+// form one pinned Split image: the rows' byte columns go to several
+// mailboxes at once (every operation is a byte-column map), each request a
+// column slice [b0, b0 + len) of every row at the image's pitch, read and
+// written in place over PCIe.  The workgroups of those mailboxes code their
+// slices side by side, so the object moves at the rate of several PCIe read
+// streams without a kernel launch or a stream synchronisation.  Slices are
+// whole 16-B vectors except the last, so no two workgroups write the same
+// bytes; the check flags are OR-ed.  A slice taken back at its deadline
+// declines the whole call (the stream path recodes every column: each
+// operation is idempotent on its outputs).
+constexpr size_t kSplitMaxShard = (size_t)64 << 10;  // objects of up to ~640 KiB at k = 10 (crossover: below)
+constexpr size_t kSplitMinSlice = 1536;             // bytes per slice at least (a lane-parallel pass)
+
+int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint8_t *img, uint32_t *bad) {
+    const int cap = std::max(2, w.nslots / 2);  // leave mailboxes to other callers
+    const int want = (int)std::min<size_t>((size_t)cap, (S + kSplitMinSlice - 1) / kSplitMinSlice);
+    int got[64], m = 0;
+    if (!w.closed.load(std::memory_order_acquire) && !w.parked.load(std::memory_order_acquire))
+        for (; m < std::max(1, want); ++m) {
+            const int i = acquire_slot(w);
+            if (i < 0) break;
+            got[m] = i;
+        }
+    if (m == 0 || (m == 1 && want > 1 && S > 4 * kSplitMinSlice)) {  // too few mailboxes free for this object
+        for (int j = 0; j < m; ++j) release_slot(w, got[j]);
+        w.declined.fetch_add(1, std::memory_order_relaxed);
+        return kWorkerDeclined;
+    }
+    const size_t slice = round_up((S + m - 1) / m, 16);
+    const int used = (int)((S + slice - 1) / slice);
+    for (int j = used; j < m; ++j) release_slot(w, got[j]);
+    m = used;
+    uint32_t rqs[64][8], ns[64];
+    for (int j = 0; j < m; ++j) {
+        const size_t b0 = (size_t)j * slice;
+        const uintptr_t p = (uintptr_t)(img + b0);
+        uint32_t *rq = rqs[j];
+        rq[kWfOp] = worker_opmask(op, mask);
+        rq[kWfShardLen] = (uint32_t)std::min(slice, S - b0);
+        rq[kWfPitch] = (uint32_t)S;
+        rq[kWfInLo] = rq[kWfOutLo] = (uint32_t)p;
+        rq[kWfInHi] = rq[kWfOutHi] = (uint32_t)(p >> 32);
+        rq[kWfSum] = worker_req_sum(rq);
+        ns[j] = post(w, got[j], rqs[j]);
+    }
+    int e = RSGPU_OK;
+    bool declined = false;
+    uint32_t any = 0;
+    for (int j = 0; j < m; ++j) {  // every slice is answered or taken back before its mailbox is freed
+        uint32_t st = 0;
+        const int r = wait_for(w, got[j], rqs[j], ns[j], st);
+        if (r == kWorkerDeclined) declined = true;
+        else if (r) e = e ? e : r;
+        else any |= st;
+    }
+    for (int j = 0; j < m; ++j) release_slot(w, got[j]);
+    if (e) return e;
+    if (declined) {
+        w.declined.fetch_add(1, std::memory_order_relaxed);
+        return kWorkerDeclined;
+    }
+    w.served.fetch_add(1, std::memory_order_relaxed);
+    *bad = any;
+    return RSGPU_OK;
+}
+
 // The worker serves one object when it can: returns RSGPU_OK with *bad set
 // (0 / 1), kWorkerDeclined to use the stream path, or an error.
 int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *const *rows, uint32_t *bad) {
@@ -912,8 +992,22 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
     // frees it only after this call is done with it
     const WorkerRef ref(ctx);
     Worker *w = ref.w;
-    if (!w || S > w->max_shard || S == 0) return kWorkerDeclined;
+    if (!w || S == 0) return kWorkerDeclined;
     const int n = ctx->n, k = ctx->k;
+    if (S > w->max_shard) {
+        // larger objects: column slices over several mailboxes, in place in
+        // one pinned Split image only (copying them would cost more than the
+        // stream path saves)
+        bool split = S <= kSplitMaxShard && S <= 0xffffffffu / (uint32_t)n;
+        for (int r = 1; r < n && split; ++r) split = rows[r] == rows[0] + (size_t)r * S;
+        const uint8_t *img = split ? (const uint8_t *)host_device_ptr(rows[0], (size_t)(n - 1) * S + (S + 15) / 16 * 16)
+                                   : nullptr;
+        if (!img) {
+            w->declined.fetch_add(1, std::memory_order_relaxed);
+            return kWorkerDeclined;
+        }
+        return worker_run_split(*w, op, S, mask, img, bad);
+    }
     const uint32_t full = (1u << n) - 1;
     // rows the op reads and writes
     uint32_t rd, wr;
@@ -955,7 +1049,7 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
         for (int r = 0; r < n; ++r)
             if ((rd >> r) & 1) std::memcpy(w->stage_h[i] + (size_t)r * S, rows[r], S);
     }
-    uint32_t rq[8] = {op, (uint32_t)S, mask, 0, (uint32_t)(uintptr_t)in, (uint32_t)((uintptr_t)in >> 32),
+    uint32_t rq[8] = {worker_opmask(op, mask), (uint32_t)S, (uint32_t)S, 0, (uint32_t)(uintptr_t)in, (uint32_t)((uintptr_t)in >> 32),
                       (uint32_t)(uintptr_t)out, (uint32_t)((uintptr_t)out >> 32)};
     rq[kWfSum] = worker_req_sum(rq);
     uint32_t status = 0;

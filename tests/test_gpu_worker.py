@@ -11,6 +11,7 @@ worker must never see stale bytes), shard sizes 1 B - 16 KiB around the
 16-B vector tails, several codes (two sub-passes for p > 4, n = 16), idle
 exit + relaunch, stop / restart, concurrent callers (declined calls take
 the stream path), objects above max_shard, and a multi-entry context."""
+import ctypes
 import threading
 import time
 
@@ -272,3 +273,108 @@ def test_worker_deadline_takes_request_back(gpu, monkeypatch):
     assert st["served"] + st["declined"] == calls, st
     assert st["declined"] > 0 and st["launches"] >= 2, st
     enc.worker_stop()
+
+
+@pytest.mark.parametrize("nslots", [16, 4])
+def test_worker_column_slices_of_large_pinned_objects(gpu, nslots):
+    """Objects past max_shard in one pinned Split image go to several
+    mailboxes as column slices at the image's pitch (worker_run_split):
+    every operation against the oracle, slices ending mid-vector (the last
+    one) and on 16-B boundaries, mismatches in the first and last slice."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start(nslots=nslots, max_shard=1024)
+    served0 = enc.worker_stats()["served"]
+    assert enc.worker_stats() == {"served": 0, "declined": 0, "launches": 0}
+    for idx, S in enumerate([1025, 4099, 6554, 33333, 65536]):
+        full = _full(k, p, S, 600 + idx)
+        buf, sh = _image(n, S, True)
+        for j in range(k):
+            sh[j][:] = full[j]
+        assert enc.EncodeVerify(sh)
+        for j in range(n):
+            assert np.array_equal(sh[j], full[j]), (S, j)
+        assert enc.worker_stats()["served"] == served0 + 1, (S, enc.worker_stats())
+        sh[k][:] = 0
+        enc.Encode(sh)
+        assert np.array_equal(sh[k], full[k]), S
+        assert enc.Verify(sh)
+        for pos in (0, S - 1):
+            sh[n - 1][pos] ^= 0x80
+            assert not enc.Verify(sh), (S, pos)
+            sh[n - 1][pos] ^= 0x80
+        # Gets on the image itself (the Go shim's route: missing rows are rows
+        # of the pinned image, rebuilt in place; *_image calls)
+        L = ia._lib.load()
+        ok = ctypes.c_int(-1)
+
+        def call(fn, present, *extra):
+            return fn(enc._ctx, buf.ctypes.data, S, n, ctypes.c_uint64(present), *extra)
+
+        def lost(*rows):
+            for j in rows:
+                sh[j][:] = 0xEE
+            return sum(1 << j for j in range(n) if j not in rows)
+
+        assert call(L.rsgpu_decode_image, lost(0, 5), ctypes.byref(ok)) == 0 and ok.value == 1, S
+        assert np.array_equal(sh[0], full[0]) and np.array_equal(sh[5], full[5]), S
+        sh[11][S - 1] ^= 1  # the extra shard wrong in the last slice only
+        assert call(L.rsgpu_decode_image, lost(3), ctypes.byref(ok)) == 0 and ok.value == 0, S
+        assert np.array_equal(sh[3], full[3]), S  # rebuilt from the first k present, as upstream
+        sh[11][S - 1] ^= 1
+        assert call(L.rsgpu_reconstruct_image, lost(1, 10), 0) == 0, S
+        assert np.array_equal(sh[1], full[1]) and np.array_equal(sh[10], full[10]), S
+        assert call(L.rsgpu_reconstruct_image, lost(2, 11), 1) == 0, S  # ReconstructData
+        assert np.array_equal(sh[2], full[2]) and np.all(sh[11] == 0xEE), S  # parity left as it was
+        sh[11][:] = full[11]
+        st = enc.worker_stats()
+        assert st["served"] - served0 == 9 and st["declined"] == 0, (S, st)  # every call above
+        served0 = st["served"]
+    # past the slices' limit (64 KiB shards): the stream path, results exact
+    S = 104858
+    full = _full(k, p, S, 699)
+    buf, sh = _image(n, S, True)
+    for j in range(k):
+        sh[j][:] = full[j]
+    assert enc.EncodeVerify(sh)
+    assert all(np.array_equal(sh[j], full[j]) for j in range(n))
+    st = enc.worker_stats()
+    assert st["served"] == served0 and st["declined"] == 1, st
+
+
+def test_worker_column_slices_beside_small_callers(gpu):
+    """Large pinned objects (column slices over several mailboxes) and 1 KiB
+    callers on one worker: slices and small requests share the mailboxes,
+    calls that find too few free take the stream path; every result exact."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start(nslots=8)
+    errors = []
+
+    def caller(tid):
+        try:
+            for i in range(20):
+                S = 50000 + 4099 * tid + 17 * i if tid < 2 else 103 + tid + i
+                full = _full(k, p, S, 2000 + tid * 100 + i)
+                buf, sh = _image(n, S, True)
+                for j in range(k):
+                    sh[j][:] = full[j]
+                assert enc.EncodeVerify(sh)
+                got = [None if j in (tid % n, (i + 3) % n) else sh[j] for j in range(n)]
+                assert enc.DecodeVerify(got)
+                for j in range(n):
+                    assert np.array_equal(got[j], full[j]), (tid, i, j)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=caller, args=(t,)) for t in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(180)
+    assert not errors, errors[:3]
+    st = enc.worker_stats()
+    assert st["served"] + st["declined"] == 6 * 20 * 2, st
+    assert st["served"] > 0

@@ -8,7 +8,8 @@
  *   [LAT_BYTES=N] [LAT_WORKER=nslots] ./lat_bench [iters [concurrent_seconds]]
  *
  * LAT_WORKER=nslots: the per-object calls go through the resident worker
- * (rsgpu_worker_start with nslots mailboxes) instead of the stream path.
+ * (rsgpu_worker_start with nslots mailboxes) instead of the stream path;
+ * LAT_MAX_SHARD sets its max_shard.
  *
  * Prints p50/p99 in microseconds for pageable (malloc) and pinned
  * (rsgpu_host_alloc) buffers.  No Python in the process. */
@@ -110,7 +111,12 @@ int main(int argc, char **argv) {
     if (rsgpu_create(k, p, 0, 0, &ctx)) return 1;
     const char *wenv = getenv("LAT_WORKER");
     if (wenv && atoi(wenv) > 0) {
-        const int e = rsgpu_worker_start(ctx, atoi(wenv), 0, S > 16384 ? S : 0);
+        /* LAT_MAX_SHARD: the worker's max_shard (default: S past 16 KiB, so
+         * one mailbox serves the whole object; 4096 or less sends larger
+         * pinned objects to several mailboxes as column slices) */
+        const char *ms = getenv("LAT_MAX_SHARD");
+        const size_t max_shard = ms ? (size_t)atol(ms) : (S > 16384 ? S : 0);
+        const int e = rsgpu_worker_start(ctx, atoi(wenv), 0, max_shard);
         printf("resident worker: %d mailboxes (rc %d)\n", atoi(wenv), e);
         if (e) return 1;
     }
