@@ -930,6 +930,15 @@ int stop_locked(rsgpu_ctx *ctx) {
 // declines the whole call (the stream path recodes every column: each
 // operation is idempotent on its outputs).
 constexpr size_t kSplitMaxShard = (size_t)64 << 10;  // objects of up to ~640 KiB at k = 10 (crossover: below)
+// RSGPU_WORKER_SPLIT_MAX (bytes per shard) overrides it: measurement
+size_t split_max_shard() {
+    static const size_t v = [] {
+        const char *e = std::getenv("RSGPU_WORKER_SPLIT_MAX");
+        const long long b = e ? std::atoll(e) : 0;
+        return b > 0 ? (size_t)b : kSplitMaxShard;
+    }();
+    return v;
+}
 constexpr size_t kSplitMinSlice = 1536;             // bytes per slice at least (a lane-parallel pass)
 
 int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint8_t *img, uint32_t *bad) {
@@ -998,7 +1007,7 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
         // larger objects: column slices over several mailboxes, in place in
         // one pinned Split image only (copying them would cost more than the
         // stream path saves)
-        bool split = S <= kSplitMaxShard && S <= 0xffffffffu / (uint32_t)n;
+        bool split = S <= split_max_shard() && S <= 0xffffffffu / (uint32_t)n;
         for (int r = 1; r < n && split; ++r) split = rows[r] == rows[0] + (size_t)r * S;
         const uint8_t *img = split ? (const uint8_t *)host_device_ptr(rows[0], (size_t)(n - 1) * S + (S + 15) / 16 * 16)
                                    : nullptr;
