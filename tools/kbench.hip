@@ -156,17 +156,23 @@ void launch_v(const void *args, dim3 grid, hipStream_t st) {
     if (NOKI) a.p.ki = 0;  // every input through the dense GF path
     unsigned nb;
     a.ord = order_for<ORD>(grid, (size_t)grid.y * a.obj_stride, nb);
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA>), dim3(nb), dim3(BS), 0, st, a);
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, LA, SA, kFormChunks>), dim3(nb), dim3(BS), 0, st, a);
 }
-// the library's launch exactly: nt loads/stores, XCD-contiguous order, and
-// the 4-workgroups-per-CU LDS occupancy cap on passes that store rows
+// the library's launch exactly: the chunk-form instantiation (kFormChunks,
+// as launch_fixed runs it), nt loads/stores, XCD-contiguous order, and the
+// LDS occupancy cap of gf_kernels.hip pass_lds (store_lds(K) workgroups per
+// CU on passes that store rows; 4 on passes that store and check rows with
+// K > 10).  Before round 4 this launched the kFormAny instantiation, whose
+// extra forms cost registers: 1-1.5 % on RS(10+2), 11 points on the RS(10+4)
+// decode with checks (profiles/r04_kbench_store_order.txt).
 template <int K, int R>
 void launch_ship(const void *args, dim3 grid, hipStream_t st) {
     ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
     unsigned nb;
     a.ord = order_for<0>(grid, 0, nb);
-    const int w = K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K);  // gf_kernels.hip store_lds
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, 2, 2>), dim3(nb), dim3(256),
+    int w = K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K);  // gf_kernels.hip store_lds
+    if (a.p.nw < (uint32_t)R && K > 10) w = 4;
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, 2, 2, kFormChunks>), dim3(nb), dim3(256),
                        a.p.nw ? 160u * 1024u / (unsigned)w - 256u : 0u, st, a);
 }
 template <int K, int R>
@@ -365,7 +371,7 @@ void launch_occ(const void *args, dim3 grid, hipStream_t st) {
     ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
     unsigned nb;
     a.ord = order_for<0>(grid, 0, nb);
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, 2, 2>), dim3(nb), dim3(BS), (160 * 1024) / W - 256, st, a);
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, U, BS, 2, 2, kFormChunks>), dim3(nb), dim3(BS), (160 * 1024) / W - 256, st, a);
 }
 
 // persistent form: W workgroups per CU (256 CUs), each walking the items of
@@ -408,7 +414,7 @@ void launch_rows(const void *args, dim3 grid, hipStream_t st) {
     }
     unsigned nb;
     a.ord = order_for<0>(grid, 0, nb);
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, 2, 2>), dim3(nb), dim3(256),
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, 2, 2, kFormChunks>), dim3(nb), dim3(256),
                        a.p.nw ? 160u * 1024u / 4u - 256u : 0u, st, a);
 }
 template <int K, int R>
@@ -437,7 +443,7 @@ void launch_small(const void *args, dim3 grid, hipStream_t st) {
     unsigned nb;
     a.ord = order_for<0>(dim3(1, (nobj + opw - 1) / opw), 0, nb);
     const int w = W > 0 ? W : (K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K));
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, LAUX, SAUX>), dim3(nb), dim3(256),
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, LAUX, SAUX, kFormChunks>), dim3(nb), dim3(256),
                        W < 0 ? 0u : 160u * 1024u / (unsigned)w - 256u, st, a);
 }
 // the LDS-staged small-object kernel (gf_apply_staged); W > 0: at most W
@@ -615,7 +621,7 @@ void launch_capp(const void *args, dim3 grid, hipStream_t st) {
     unsigned nb;
     a.ord = order_for<0>(grid, 0, nb);
     const int w = K <= 5 ? 8 : (40 / K < 2 ? 2 : 40 / K);
-    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, LA, SA>), dim3(nb), dim3(256),
+    hipLaunchKernelGGL((gf_apply_kernel<K, R, 1, 256, LA, SA, kFormChunks>), dim3(nb), dim3(256),
                        a.p.nw ? 160u * 1024u / (unsigned)w - 256u : 0u, st, a);
 }
 template <int K, int R>
