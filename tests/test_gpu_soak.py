@@ -18,7 +18,11 @@ than tests/test_gpu_random.py:
     codes of <= 16 shards, shards up to 16 KiB) and variable-size device
     tables (rsgpu_*_dev_objs: encode, Verify flags, fused decode,
     ReconstructData over objects of different sizes and pitches); device
-    masks of 17-32-shard codes (no atlas: masks read back, host-planned).
+    masks of 17-32-shard codes (no atlas: masks read back, host-planned);
+  * round 4: worker objects past max_shard in pinned Split images (column
+    slices over several mailboxes, shards up to 64 KiB) and host ops coded in
+    column slabs (RSGPU_SLAB_BYTES drawn small, so objects of a few KB take
+    several slabs).
 Every result is compared bit-exact (bytes) or exactly (booleans, error
 classes) with the oracle on the same input.  Prints a per-kind case count."""
 import collections
@@ -374,7 +378,7 @@ def _worker_case(rng, counts):
     k = int(rng.integers(1, 14))
     p = int(rng.integers(1, min(5, 16 - k) + 1))
     n = k + p
-    size = _size(rng, 16384)
+    size = _size(rng, 16384 if rng.random() < 0.7 else 65536)
     kind = str(rng.choice(["vandermonde", "cauchy"]))
     enc = _worker_enc(k, p, kind)
     data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
@@ -499,6 +503,16 @@ def _objs_case(rng, counts):
                 assert np.array_equal(a, coded[o + i * pitch: o + i * pitch + S]), (tag, op, lost, i)
 
 
+def _slab_case(rng, counts):
+    """a host op with a small slab size: the object is coded in column slabs"""
+    os.environ["RSGPU_SLAB_BYTES"] = str(int(rng.integers(4096, 1 << 16)))
+    try:
+        _host_case(rng, counts)
+        counts["slabs"] += 1
+    finally:
+        del os.environ["RSGPU_SLAB_BYTES"]
+
+
 def test_gpu_soak_vs_oracle(gpu):
     seed = int(os.environ.get("RSGPU_SOAK_SEED", "20261016"))
     rng = np.random.default_rng(seed)
@@ -516,10 +530,12 @@ def test_gpu_soak_vs_oracle(gpu):
             _shard_major_case(rng, counts)
         elif r < 0.76:
             _pinned_case(rng, counts)
-        elif r < 0.9:
+        elif r < 0.88:
             _worker_case(rng, counts)
-        else:
+        elif r < 0.94:
             _objs_case(rng, counts)
+        else:
+            _slab_case(rng, counts)
         if time.time() - last > 30:  # progress line (a silent GPU run reads as hung)
             last = time.time()
             print(f"soak {last - t0:.0f}s: {sum(counts.values())} cases", flush=True)
