@@ -340,6 +340,66 @@ def pmc_traffic(kernel_key, workload, alg_bytes):
         return None, f"none: no committed PMC summary for {kernel_key}"
 
 
+def under_profiler() -> bool:
+    """True when this process runs under rocprofv3 (its tool library is
+    preloaded): a child rocprofv3 run would nest profilers."""
+    return any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ) or \
+        "rocprof" in os.environ.get("LD_PRELOAD", "")
+
+
+def pmc_traffic_live(args, kernel_key, alg_bytes):
+    """HBM bytes per launch of `kernel_key` measured in THIS run: two child
+    runs of this same workload (3 warm-up + 3 timed steps, same batch
+    rotation) under `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
+    (separate passes: the TCC block cannot hold both, MI355X_MICROARCH.md
+    §rocprofv3 PMC slots), each averaged over that kernel's dispatches;
+    read = 2 x FETCH_SIZE (the gfx950 correction of MI355X_MICROARCH.md
+    §HBM), write = WRITE_SIZE, both KiB.  The children are separate processes
+    started after this one's timed region (never an exec), each under a
+    time limit; returns (bytes or None, source note)."""
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not on PATH"
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import per_kernel, short
+    key = short(kernel_key)
+    got = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = [exe, "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--no-cpu", "--no-pmc",
+               "--steps", "3", "--warmup", "3", "--copies", str(args.copies)]
+        if args.batch:
+            cmd += ["--batch", str(args.batch)]
+        p = subprocess.Popen(cmd, env=dict(os.environ, BENCH_PMC_CHILD="1"), stdout=subprocess.DEVNULL,
+                             stderr=subprocess.DEVNULL, start_new_session=True)
+        try:
+            rc = p.wait(timeout=180)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)  # a refused counter set hangs past SIGTERM
+            p.wait()
+            return None, f"rocprofv3 --pmc {counter} pass timed out (180 s)"
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if rc != 0 or not files:
+            return None, f"rocprofv3 --pmc {counter} pass failed (rc {rc})"
+        val = per_kernel(files[0], counter).get(key)
+        shutil.rmtree(out, ignore_errors=True)
+        if not val:
+            return None, f"rocprofv3 --pmc {counter}: no dispatch of {key}"
+        got[counter] = val
+    rd = 2.0 * got["FETCH_SIZE"][0] * 1024
+    wr = got["WRITE_SIZE"][0] * 1024
+    return int(rd + wr), (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes of this "
+                          f"workload ({got['FETCH_SIZE'][1]} / {got['WRITE_SIZE'][1]} dispatches of {key}), "
+                          f"read 2 x FETCH_SIZE = {int(rd)} B + write {int(wr)} B per launch, "
+                          f"{(rd + wr) / alg_bytes:.4f} x algorithmic")
+
+
 def run_trace(args):
     """BASELINE config 5: mixed 4 KiB-100 MiB objects (log-uniform, numpy
     PCG64 seed 20200225, 512 objects, ~5 GiB), RS(10+2), one MI355X, host <->
@@ -597,6 +657,9 @@ def main():
                     help="also time K steps re-coding one batch (warm Infinity Cache; comparison only)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="take roofline.traffic from the committed PMC summary instead of two rocprofv3 "
+                         "--pmc child passes of this workload (the default at N = 1 when rocprofv3 is present)")
     args = ap.parse_args()
     if args.warmup is None:
         # ~0.1-0.2 s of untimed steps: the HBM-bound workloads time the same
@@ -858,7 +921,19 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     # every rank's own kernel rate (N > 1: each GPU codes its own objects)
     frac_ranks = [round(a / HBM_PEAK_GBS, 4) for a in dctx.gather(achieved)]
-    traffic, traffic_src = pmc_traffic(kernel_key, args.workload, dom_bytes)
+    traffic, traffic_src = None, None
+    # HBM traffic of the dominant kernel measured in this run (rank 0 of a
+    # one-GPU run; N > 1 ranks and profiled runs use the committed summary)
+    if world == 1 and not args.no_pmc and not os.environ.get("BENCH_PMC_CHILD") and "+" not in kernel_key \
+            and not under_profiler():
+        traffic, traffic_src = pmc_traffic_live(args, kernel_key, dom_bytes)
+        if traffic is None:
+            log(f"PMC traffic not measured: {traffic_src}")
+            note = traffic_src
+            traffic, traffic_src = pmc_traffic(kernel_key, args.workload, dom_bytes)
+            traffic_src = f"{traffic_src} (live passes: {note})"
+    if traffic_src is None:
+        traffic, traffic_src = pmc_traffic(kernel_key, args.workload, dom_bytes)
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
