@@ -165,9 +165,10 @@ int rsgpu_update(rsgpu_ctx *ctx, uint8_t *const *shards, const size_t *lens, int
  * pinned image (memcpy).  Objects with shard_len > max_shard (up to 64 KiB)
  * whose rows form one pinned Split image go to several free mailboxes at once,
  * each coding a column slice of every row in place (128-640 KiB objects:
- * 1.1-1.4x faster than the stream path).  Larger or pageable objects past
- * max_shard, codes of more than 16 shards, and calls that find every mailbox
- * busy take the stream path.
+ * 1.1-1.4x faster than the stream path); other buffers with shard_len up to
+ * 16 KiB go as slices staged through the mailboxes' images.  Larger objects,
+ * codes of more than 16 shards, and calls that find too few mailboxes free
+ * take the stream path.
  * Results, checks and errors are exactly those of the stream path.
  *   nslots     mailboxes = resident workgroups (1..64; 0: 8)
  *   idle_us    the kernel leaves after this long without any request (0: 50 ms)

@@ -940,18 +940,39 @@ size_t split_max_shard() {
     return v;
 }
 constexpr size_t kSplitMinSlice = 1536;             // bytes per slice at least (a lane-parallel pass)
+// staged slices (pageable rows copied into the mailboxes' images): up to 16
+// KiB shards.  Past it the copies through the BAR cost more than the launch
+// the worker saves: pageable 256 KiB decode 24.2 us stream vs 31.5 us staged,
+// 640 KiB 37.9 vs 76.0 (64 KiB 18.7 -> 13.1, 128 KiB 20.0 -> 16.3;
+// profiles/r04_worker_split/staged_*)
+constexpr size_t kStagedSplitMaxShard = (size_t)16 << 10;
 
-int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint8_t *img, uint32_t *bad) {
-    const int cap = std::max(2, w.nslots / 2);  // leave mailboxes to other callers
-    const int want = (int)std::min<size_t>((size_t)cap, (S + kSplitMinSlice - 1) / kSplitMinSlice);
+// Two forms.  In place (img: the device view of one pinned Split image):
+// each slice is read and written there at the image's pitch.  Staged (img ==
+// nullptr: pageable rows, e.g. the Go Split array an EcSet passes): each
+// slice's input rows are copied into its mailbox's image (VRAM through the
+// BAR, or pinned host memory) at pitch = slice length, the written rows come
+// back through the mailbox's pinned image; slices then fit max_shard, so
+// this form may take every mailbox.  rd / wr: the rows the op reads / writes.
+int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint8_t *img, uint8_t *const *rows,
+                     int n, uint32_t rd, uint32_t wr, uint32_t *bad) {
+    const bool staged = img == nullptr;
+    if (staged && S > kStagedSplitMaxShard) {
+        w.declined.fetch_add(1, std::memory_order_relaxed);
+        return kWorkerDeclined;
+    }
+    const size_t smax = w.max_shard & ~(size_t)15;  // a staged slice fits its mailbox's image
+    const int need = staged ? (int)((S + smax - 1) / smax) : 1;
+    const int cap = staged ? w.nslots : std::max(2, w.nslots / 2);  // in place: leave mailboxes to other callers
+    const int want = std::max(need, (int)std::min<size_t>((size_t)cap, (S + kSplitMinSlice - 1) / kSplitMinSlice));
     int got[64], m = 0;
-    if (!w.closed.load(std::memory_order_acquire) && !w.parked.load(std::memory_order_acquire))
-        for (; m < std::max(1, want); ++m) {
+    if (want <= cap && !w.closed.load(std::memory_order_acquire) && !w.parked.load(std::memory_order_acquire))
+        for (; m < want; ++m) {
             const int i = acquire_slot(w);
             if (i < 0) break;
             got[m] = i;
         }
-    if (m == 0 || (m == 1 && want > 1 && S > 4 * kSplitMinSlice)) {  // too few mailboxes free for this object
+    if (m < need || m == 0 || (m == 1 && want > 1 && S > 4 * kSplitMinSlice)) {  // too few mailboxes free
         for (int j = 0; j < m; ++j) release_slot(w, got[j]);
         w.declined.fetch_add(1, std::memory_order_relaxed);
         return kWorkerDeclined;
@@ -962,16 +983,29 @@ int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint
     m = used;
     uint32_t rqs[64][8], ns[64];
     for (int j = 0; j < m; ++j) {
-        const size_t b0 = (size_t)j * slice;
-        const uintptr_t p = (uintptr_t)(img + b0);
+        const int i = got[j];
+        const size_t b0 = (size_t)j * slice, len = std::min(slice, S - b0);
+        uintptr_t pin = (uintptr_t)(img + b0), pout = pin;
+        size_t pitch = S;
+        if (staged) {
+            uint8_t *dst = w.vram ? w.v_img[i] : w.stage_h[i];
+            for (int r = 0; r < n; ++r)
+                if ((rd >> r) & 1) std::memcpy(dst + (size_t)r * len, rows[r] + b0, len);
+            if (w.vram) __builtin_ia32_sfence();  // the rows before the request line (post_line)
+            pin = (uintptr_t)(w.vram ? w.v_img[i] : w.stage_d[i]);
+            pout = wr ? (uintptr_t)w.stage_d[i] : pin;
+            pitch = len;
+        }
         uint32_t *rq = rqs[j];
         rq[kWfOp] = worker_opmask(op, mask);
-        rq[kWfShardLen] = (uint32_t)std::min(slice, S - b0);
-        rq[kWfPitch] = (uint32_t)S;
-        rq[kWfInLo] = rq[kWfOutLo] = (uint32_t)p;
-        rq[kWfInHi] = rq[kWfOutHi] = (uint32_t)(p >> 32);
+        rq[kWfShardLen] = (uint32_t)len;
+        rq[kWfPitch] = (uint32_t)pitch;
+        rq[kWfInLo] = (uint32_t)pin;
+        rq[kWfInHi] = (uint32_t)(pin >> 32);
+        rq[kWfOutLo] = (uint32_t)pout;
+        rq[kWfOutHi] = (uint32_t)(pout >> 32);
         rq[kWfSum] = worker_req_sum(rq);
-        ns[j] = post(w, got[j], rqs[j]);
+        ns[j] = post(w, i, rqs[j]);
     }
     int e = RSGPU_OK;
     bool declined = false;
@@ -983,6 +1017,12 @@ int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint
         else if (r) e = e ? e : r;
         else any |= st;
     }
+    if (staged && !e && !declined)  // the written rows back to the caller's buffers
+        for (int j = 0; j < m; ++j) {
+            const size_t b0 = (size_t)j * slice, len = std::min(slice, S - b0);
+            for (int r = 0; r < n; ++r)
+                if ((wr >> r) & 1) std::memcpy(rows[r] + b0, w.stage_h[got[j]] + (size_t)r * len, len);
+        }
     for (int j = 0; j < m; ++j) release_slot(w, got[j]);
     if (e) return e;
     if (declined) {
@@ -1003,20 +1043,6 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
     Worker *w = ref.w;
     if (!w || S == 0) return kWorkerDeclined;
     const int n = ctx->n, k = ctx->k;
-    if (S > w->max_shard) {
-        // larger objects: column slices over several mailboxes, in place in
-        // one pinned Split image only (copying them would cost more than the
-        // stream path saves)
-        bool split = S <= split_max_shard() && S <= 0xffffffffu / (uint32_t)n;
-        for (int r = 1; r < n && split; ++r) split = rows[r] == rows[0] + (size_t)r * S;
-        const uint8_t *img = split ? (const uint8_t *)host_device_ptr(rows[0], (size_t)(n - 1) * S + (S + 15) / 16 * 16)
-                                   : nullptr;
-        if (!img) {
-            w->declined.fetch_add(1, std::memory_order_relaxed);
-            return kWorkerDeclined;
-        }
-        return worker_run_split(*w, op, S, mask, img, bad);
-    }
     const uint32_t full = (1u << n) - 1;
     // rows the op reads and writes
     uint32_t rd, wr;
@@ -1025,6 +1051,19 @@ int worker_run(rsgpu_ctx *ctx, uint32_t op, size_t S, uint32_t mask, uint8_t *co
         case kWopVerify: rd = full; wr = 0; break;
         case kWopReconstructData: rd = mask; wr = ~mask & ((1u << k) - 1); break;
         default: rd = mask; wr = ~mask & full; break;
+    }
+    if (S > w->max_shard) {
+        // larger objects: column slices over several mailboxes, in place in
+        // one pinned Split image, else staged through the mailboxes' images
+        if (S > split_max_shard() || S > 0xffffffffu / (uint32_t)n) {
+            w->declined.fetch_add(1, std::memory_order_relaxed);
+            return kWorkerDeclined;
+        }
+        bool split = true;
+        for (int r = 1; r < n && split; ++r) split = rows[r] == rows[0] + (size_t)r * S;
+        const uint8_t *img = split ? (const uint8_t *)host_device_ptr(rows[0], (size_t)(n - 1) * S + (S + 15) / 16 * 16)
+                                   : nullptr;
+        return worker_run_split(*w, op, S, mask, img, rows, n, rd, wr, bad);
     }
     // stopped or parked: decline (checked before and after taking a mailbox;
     // a stop / park takes every mailbox, so one of the two checks sees it)

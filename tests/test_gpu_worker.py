@@ -174,15 +174,23 @@ def test_worker_idle_exit_relaunch_and_stop(gpu):
 
 
 def test_worker_large_shards_take_stream_path(gpu):
+    """Past the column slices' limit (64 KiB shards) every object takes the
+    stream path, pinned or pageable; pageable objects past max_shard but
+    within it go to several mailboxes through their images (staged slices)."""
     k, p = 10, 2
     n = k + p
     enc = ia.New(k, p)
     enc.worker_start(max_shard=4096)
-    full = _full(k, p, 9000, 9)
-    sh = [full[j].copy() if j < k else np.zeros(9000, np.uint8) for j in range(n)]
+    full = _full(k, p, 70000, 9)
+    sh = [full[j].copy() if j < k else np.zeros(70000, np.uint8) for j in range(n)]
     assert enc.EncodeVerify(sh)
     assert np.array_equal(sh[k], full[k])
     assert enc.worker_stats()["served"] == 0
+    full = _full(k, p, 9000, 10)
+    sh = [full[j].copy() if j < k else np.zeros(9000, np.uint8) for j in range(n)]
+    assert enc.EncodeVerify(sh)
+    assert all(np.array_equal(sh[j], full[j]) for j in range(n))
+    assert enc.worker_stats()["served"] == 1
 
 
 def test_worker_concurrent_callers(gpu):
@@ -273,6 +281,50 @@ def test_worker_deadline_takes_request_back(gpu, monkeypatch):
     assert st["served"] + st["declined"] == calls, st
     assert st["declined"] > 0 and st["launches"] >= 2, st
     enc.worker_stop()
+
+
+@pytest.mark.parametrize("nslots,max_shard", [(16, 4096), (8, 16384)])
+def test_worker_staged_column_slices_pageable(gpu, nslots, max_shard):
+    """Pageable objects past max_shard (the Go Split array an EcSet passes):
+    staged column slices, every operation through the mirror (missing rows
+    are fresh buffers), against the oracle."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p)
+    enc.worker_start(nslots=nslots, max_shard=max_shard)
+    served = declined = 0
+    for idx, S in enumerate([max_shard + 1, 9000, 16384, 26215]):
+        full = _full(k, p, S, 800 + idx)
+        sh = [full[j].copy() if j < k else np.full(S, 0x33, np.uint8) for j in range(n)]
+        assert enc.EncodeVerify(sh), S
+        assert all(np.array_equal(sh[j], full[j]) for j in range(n)), S
+        sh[k + 1][:] = 0
+        enc.Encode(sh)
+        assert np.array_equal(sh[k + 1], full[k + 1]), S
+        assert enc.Verify(sh), S
+        sh[k][S - 1] ^= 4
+        assert not enc.Verify(sh), S
+        sh[k][S - 1] ^= 4
+        got = [None if j in (0, 5) else sh[j] for j in range(n)]
+        assert enc.DecodeVerify(got), S
+        assert np.array_equal(got[0], full[0]) and np.array_equal(got[5], full[5]), S
+        bad = [None if j == 7 else sh[j] for j in range(n)]
+        bad[11] = bad[11].copy()
+        bad[11][0] ^= 1
+        assert not enc.DecodeVerify(bad), S
+        assert np.array_equal(bad[7], full[7]), S
+        got = [None if j in (2, 11) else sh[j] for j in range(n)]
+        enc.ReconstructData(got)
+        assert np.array_equal(got[2], full[2]) and got[11] is None, S
+        got = [None if j in (3, 10) else sh[j] for j in range(n)]
+        enc.Reconstruct(got)
+        assert np.array_equal(got[3], full[3]) and np.array_equal(got[10], full[10]), S
+        st = enc.worker_stats()
+        if S <= 16384:  # staged slices (up to 16 KiB shards): every call above served
+            assert st["served"] - served == 8 and st["declined"] == declined, (S, st)
+        else:  # past it: the stream path
+            assert st["served"] == served, (S, st)
+        served, declined = st["served"], st["declined"]
 
 
 @pytest.mark.parametrize("nslots", [16, 4])
