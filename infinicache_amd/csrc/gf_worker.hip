@@ -957,7 +957,7 @@ constexpr size_t kStagedSplitMaxShard = (size_t)16 << 10;
 int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint8_t *img, uint8_t *const *rows,
                      int n, uint32_t rd, uint32_t wr, uint32_t *bad) {
     const bool staged = img == nullptr;
-    if (staged && S > kStagedSplitMaxShard) {
+    if (staged && (S > kStagedSplitMaxShard || w.max_shard < 16)) {
         w.declined.fetch_add(1, std::memory_order_relaxed);
         return kWorkerDeclined;
     }

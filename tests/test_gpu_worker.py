@@ -430,3 +430,26 @@ def test_worker_column_slices_beside_small_callers(gpu):
     st = enc.worker_stats()
     assert st["served"] + st["declined"] == 6 * 20 * 2, st
     assert st["served"] > 0
+
+
+def test_worker_slices_on_multi_entry_context(gpu):
+    """Column slices through a multi-entry context (per-object calls go to
+    the entries round-robin, each entry its own worker): pinned images and
+    pageable buffers past max_shard, every result exact, every entry used."""
+    k, p = 10, 2
+    n = k + p
+    enc = ia.New(k, p, devices=[0, 0])
+    enc.worker_start(nslots=8, max_shard=2048)
+    for i, (S, pinned) in enumerate([(20000, True), (9000, False), (50001, True), (16000, False)] * 2):
+        full = _full(k, p, S, 900 + i)
+        buf, sh = _image(n, S, pinned)
+        for j in range(k):
+            sh[j][:] = full[j]
+        assert enc.EncodeVerify(sh), (S, pinned)
+        assert all(np.array_equal(sh[j], full[j]) for j in range(n)), (S, pinned)
+        got = [None if j in (i % n, (i + 7) % n) else sh[j] for j in range(n)]
+        assert enc.DecodeVerify(got), (S, pinned)
+        assert all(np.array_equal(got[j], full[j]) for j in range(n)), (S, pinned)
+    st = enc.worker_stats()
+    assert st["served"] >= 8, st
+    assert all(c > 0 for c in enc.device_calls()), enc.device_calls()
