@@ -195,10 +195,11 @@ int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_
  * the stream path); the per-object calls go back to the stream path.
  * rsgpu_destroy stops it too. */
 int rsgpu_worker_stop(rsgpu_ctx *ctx);
-/* Calls the worker served, calls it declined because every mailbox was busy
- * (they took the stream path), and kernel launches so far (the first call
- * after an idle exit relaunches it); summed over a multi-device context's
- * entries.  Any pointer may be NULL. */
+/* Calls the worker served, calls it declined (too few mailboxes free, an
+ * object past max_shard it cannot slice, a request taken back at its
+ * deadline: they took the stream path), and kernel launches so far (the
+ * first call after an idle exit relaunches it); summed over a multi-device
+ * context's entries.  Any pointer may be NULL. */
 int rsgpu_worker_stats(const rsgpu_ctx *ctx, uint64_t *served, uint64_t *declined, uint64_t *launches);
 
 /* ---- per-object calls on one contiguous image ----------------------------
