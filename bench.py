@@ -379,11 +379,11 @@ def pmc_traffic_live(args, kernel_key, alg_bytes):
         p = subprocess.Popen(cmd, env=dict(os.environ, BENCH_PMC_CHILD="1"), stdout=subprocess.DEVNULL,
                              stderr=subprocess.DEVNULL, start_new_session=True)
         try:
-            rc = p.wait(timeout=180)
+            rc = p.wait(timeout=90)
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)  # a refused counter set hangs past SIGTERM
             p.wait()
-            return None, f"rocprofv3 --pmc {counter} pass timed out (180 s)"
+            return None, f"rocprofv3 --pmc {counter} pass timed out (90 s)"
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if rc != 0 or not files:
             return None, f"rocprofv3 --pmc {counter} pass failed (rc {rc})"
