@@ -230,8 +230,12 @@ int rsgpu_decode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nsha
  *     object whose shard is the whole row: the gap bytes are pad bytes and
  *     are overwritten in written rows, as are the row's bytes up to
  *     roundup16 of its last piece's end when the pitch holds them.
- * (data+parity)*pitch < 4 GiB; any alignment (16-B aligned d_base, pitch and
- * obj_stride are the fast path and are required by the *_dev_masks calls).
+ * Any alignment (16-B aligned d_base, pitch and obj_stride are the fast path
+ * and are required by the *_dev_masks calls).  Object size: the uniform
+ * calls (rsgpu_{encode,verify,reconstruct,decode}_dev) take objects whose
+ * rows span 4 GiB or more too, coded in column slabs through a scratch image
+ * (two extra device copies per slab); the mixed-pattern calls require
+ * (data+parity)*pitch < 4 GiB.
  * Kernels read whole 16-B vectors and write them where the layout allows:
  * written rows' bytes in [shard_len, min(space, roundup16(shard_len))), space
  * = the pitch (object-major) or obj_stride (shard-major), are overwritten

@@ -883,10 +883,44 @@ hipError_t launch_last_object(Plan &p, const Layout &L, uint32_t *d_bad, hipStre
     return e != hipSuccess ? e : f;
 }
 
+// Objects whose rows span 4 GiB or more (the 32-bit offsets of a pass's
+// buffer resource cannot reach them): every operation is a byte-column map,
+// so each object is coded in column slabs — the slab's rows gathered into a
+// stream-ordered scratch image (one 2D copy, 16-B pitch, <= 1 GiB), the pass
+// run there, the written rows' slab bytes copied back.  Check flags: the
+// caller's memset precedes (check plans OR into d_bad[o]); plans without
+// checks clear d_bad[o] in every slab alike.  Device-to-device copies move
+// each slab twice, so these objects code at a fraction of the pass's rate.
+hipError_t launch_huge(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
+    const size_t nrows = rows_extent(p, 1);
+    const size_t lim = (size_t)1 << 30;
+    const size_t slab = std::max<size_t>(4096, (lim / nrows) & ~(size_t)4095);
+    uint8_t *tmp = nullptr;
+    hipError_t e = hipMallocAsync((void **)&tmp, nrows * slab + 64, st);
+    if (e != hipSuccess) return e;
+    for (int o = 0; o < L.nobj && e == hipSuccess; ++o) {
+        uint8_t *obj = L.base + (size_t)o * L.obj_stride;
+        for (size_t b0 = 0; b0 < L.shard_len && e == hipSuccess; b0 += slab) {
+            const size_t len = std::min(slab, L.shard_len - b0), P = (len + 15) / 16 * 16;
+            e = hipMemcpy2DAsync(tmp, P, obj + b0, L.pitch, len, nrows, hipMemcpyDeviceToDevice, st);
+            Layout one{tmp, 0, P, len, 1};
+            one.slack = true;
+            if (e == hipSuccess) e = launch_plan_core(p, one, d_bad ? d_bad + o : nullptr, st);
+            for (int r = 0; r < p.nw && e == hipSuccess; ++r)
+                e = hipMemcpyAsync(obj + (size_t)p.out_rows[r] * L.pitch + b0, tmp + (size_t)p.out_rows[r] * P, len,
+                                   hipMemcpyDeviceToDevice, st);
+        }
+    }
+    const hipError_t f = hipFreeAsync(tmp, st);
+    return e != hipSuccess ? e : f;
+}
+
 }  // namespace
 
 hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
     if (L.nobj <= 0 || p.R <= 0) return hipSuccess;
+    if (!L.in_base && !L.out_base && L.sub_stride == 0 && rows_extent(p, L.pitch) + 16 >= ((size_t)1 << 32))
+        return launch_huge(p, L, d_bad, st);
     // Shard-major batch ([shard][object]: shard i of object o at
     // base + i*pitch + o*obj_stride, the objects' pieces of one shard back to
     // back): coding is byte-position-wise, so the batch IS one object whose

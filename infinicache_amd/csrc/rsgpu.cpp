@@ -454,15 +454,17 @@ int upload_atlas(rsgpu_ctx *ctx, const Atlas &H, Atlas &D) {
     return RSGPU_OK;
 }
 
+// huge: the caller codes objects whose rows span 4 GiB or more (launch_plan
+// codes them in column slabs); the mixed-pattern calls do not
 int check_layout(const rsgpu_ctx *ctx, const void *base, size_t shard_len, size_t pitch,
-                 size_t obj_stride, int nobj) {
+                 size_t obj_stride, int nobj, bool huge = false) {
     if (!base || nobj < 0) return RSGPU_ERR_INVALID_ARG;
     if (shard_len == 0) return RSGPU_ERR_SHARD_NO_DATA;
     // any alignment: a pitch below 16 * ceil(S / 16) stores the last vector
     // of a row in 8/4/2/1-byte pieces (store_row); 16-B aligned rows and
     // objects are the fast path
     if (pitch < shard_len) return RSGPU_ERR_INVALID_ARG;
-    if ((size_t)ctx->n * pitch >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
+    if (!huge && (size_t)ctx->n * pitch >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
     // objects must not overlap: object-major ([object][shard]: each object's
     // rows within its stride) or shard-major ([shard][object]: each shard row
     // holds every object's piece)
@@ -1016,7 +1018,7 @@ int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitc
                      size_t obj_stride, int nobj, void *stream) {
     RSGPU_FORWARD_DEV(rsgpu_encode_dev, d_base, d_base, shard_len, pitch, obj_stride, nobj, stream)
     if (!ctx) return RSGPU_ERR_INVALID_ARG;
-    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj, true);
     if (e) return e;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
@@ -1030,7 +1032,7 @@ int rsgpu_verify_dev(rsgpu_ctx *ctx, const void *d_base, size_t shard_len, size_
                      size_t obj_stride, int nobj, uint32_t *d_bad, void *stream) {
     RSGPU_FORWARD_DEV(rsgpu_verify_dev, d_base, d_base, shard_len, pitch, obj_stride, nobj, d_bad, stream)
     if (!ctx || !d_bad) return RSGPU_ERR_INVALID_ARG;
-    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj, true);
     if (e) return e;
     DeviceGuard dg_;
     if ((e = ctx->use_device(dg_))) return e;
@@ -1045,7 +1047,7 @@ static int recon_dev(rsgpu_ctx *ctx, void *d_base, const uint8_t *present, size_
                      size_t pitch, size_t obj_stride, int nobj, bool data_only, bool check,
                      uint32_t *d_bad, void *stream) {
     if (!ctx || !present) return RSGPU_ERR_INVALID_ARG;
-    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj);
+    int e = check_layout(ctx, d_base, shard_len, pitch, obj_stride, nobj, true);
     if (e) return e;
     int np = 0;
     for (int i = 0; i < ctx->n; ++i) np += present[i] != 0;
