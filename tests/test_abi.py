@@ -135,6 +135,14 @@ def test_device_layout_validation():
     # the device-resolved mixed-pattern calls need 16-B aligned rows
     with pytest.raises(ia.InvalidArgument):
         enc.decode_dev_masks(4096, 8192, 100, 100, 12 * 100, 1, 16384)
+    # rows spanning 4 GiB or more: a valid layout for the uniform calls
+    # (coded in column slabs, launch_huge), not for the mixed-pattern ones
+    big = 400 << 20
+    if not ia.device_ok(0):
+        with pytest.raises(ia.NoDevice):
+            enc.encode_dev(4096, big, big, 12 * big, 1)
+    with pytest.raises(ia.InvalidArgument):
+        enc.decode_dev_masks(4096, 8192, big, big, 12 * big, 1, 16384)
 
 
 @pytest.mark.parametrize("k,p", [(10, 2), (10, 4), (6, 3), (40, 20), (200, 50)])
