@@ -242,7 +242,11 @@ int rsgpu_decode_image(rsgpu_ctx *ctx, uint8_t *base, size_t shard_len, int nsha
  * with the coding of the input rows' pad bytes (zero when those are zero);
  * with less space (e.g. pitch = shard_len, byte-packed rows) nothing past
  * shard_len is written.  `stream` is a hipStream_t (NULL = default stream);
- * calls are asynchronous on it and make no host<->device synchronisation. */
+ * calls are asynchronous on it and make no host<->device synchronisation.
+ * HIP graphs: once a first call has built the code's plans (and, for the
+ * *_dev_masks calls, the pattern atlas), rsgpu_{encode,verify,reconstruct,
+ * decode}_dev and rsgpu_*_dev_masks issue only stream-ordered work and may be
+ * captured into a graph and replayed (tests/test_gpu_graphs.py). */
 
 /* Encode nobj objects: rows [k, k+p) <- M[k:] x rows [0, k). */
 int rsgpu_encode_dev(rsgpu_ctx *ctx, void *d_base, size_t shard_len, size_t pitch,

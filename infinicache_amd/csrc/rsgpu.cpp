@@ -553,6 +553,21 @@ int run_masked(rsgpu_ctx *ctx, const AtlasView &A, AtlasMode mode, const Layout 
         HIP_TRY(launch_masked(A, L, d_masks, d_status, nullptr, nullptr, st));
         return RSGPU_OK;
     }
+    // Inside a stream capture (a HIP graph): the scratch ring's event waits
+    // and first-use allocations are not capturable, and a replay must not
+    // share a ring slot with later calls; the counters then come from a
+    // stream-ordered allocation the graph owns (alloc + memset + free nodes)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) {
+        uint32_t *tmp = nullptr;
+        HIP_TRY(hipMallocAsync((void **)&tmp, (size_t)L.nobj * 2 * sizeof(uint32_t), st));
+        hipError_t e = hipMemsetAsync(tmp, 0, (size_t)L.nobj * 2 * sizeof(uint32_t), st);
+        if (e == hipSuccess) e = launch_masked(A, L, d_masks, d_status, tmp, tmp + L.nobj, st);
+        const hipError_t f = hipFreeAsync(tmp, st);
+        if (e != hipSuccess) return hip_fail(e, "launch_masked (capture)");
+        if (f != hipSuccess) return hip_fail(f, "status scratch (capture)");
+        return RSGPU_OK;
+    }
     StatusScratch::Slot *sc = nullptr;
     HIP_TRY(ctx->scratch.acquire((size_t)L.nobj, st, sc));
     const hipError_t e = launch_masked(A, L, d_masks, d_status, sc->d, sc->d + sc->cap, st);
