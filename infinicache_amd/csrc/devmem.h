@@ -19,4 +19,13 @@ void drain_retired();
 // returns when the bytes have landed
 hipError_t upload(void *dst, const void *src, size_t bytes);
 
+// host memory copies of a per-object call's rows (hostcopy.cpp): large
+// batches are spread over a small thread pool, small ones are one memcpy
+struct CopyJob {
+    void *dst;
+    const void *src;
+    size_t len;
+};
+void copy_rows(const CopyJob *jobs, size_t n);
+
 }  // namespace rsgpu

@@ -217,7 +217,9 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
             i = j;
         }
     } else {
-        for (int c = 0; c < plan.K; ++c) std::memcpy(s->h + (size_t)plan.in_rows[c] * size, in_src[c], size);
+        std::vector<CopyJob> cp((size_t)plan.K);
+        for (int c = 0; c < plan.K; ++c) cp[c] = {s->h + (size_t)plan.in_rows[c] * size, in_src[c], size};
+        copy_rows(cp.data(), cp.size());
         if (plan.K <= kRedirectMaxK && s->hdev) {
             // the pass reads the pinned staging image in place (zero-copy);
             // the slot holds nrows_staged*size + 16 bytes at least
@@ -285,8 +287,11 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         ctx->put_slot(std::move(s));
         return hip_fail(he, "run_host");
     }
-    if (!pin_out)
-        for (int r = 0; r < plan.nw; ++r) std::memcpy(out_dst[r], s->h + (size_t)orows[r] * size, size);
+    if (!pin_out) {
+        std::vector<CopyJob> cp((size_t)plan.nw);
+        for (int r = 0; r < plan.nw; ++r) cp[r] = {out_dst[r], s->h + (size_t)orows[r] * size, size};
+        copy_rows(cp.data(), cp.size());
+    }
     if (bad) *bad = plan.nw < plan.R ? *s->h_bad : 0;
     if (then_bad) *then_bad = *s->h_bad;
     ctx->put_slot(std::move(s));
