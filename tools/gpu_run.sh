@@ -29,6 +29,20 @@ for s in $STEPS; do
             run bench_enc 300 python bench.py --workload enc --no-cpu
             run bench_dec4 300 python bench.py --workload dec4 --no-cpu
             run bench_mixed 300 python bench.py --workload encdec_mixed --no-cpu ;;
+    allwl)  # every device-resident workload once (value, frac, per-op kernel ms, decode check)
+            for wl in ${ALL_WLS:-enc dec4 encdec_mixed encdec_upstream small small_mixed small1k small1k_sm small1k_sm_mixed_a128 wide}; do
+              run wl_$wl 300 python bench.py --workload $wl --no-cpu --no-pmc
+            done
+            run wl_trace 600 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu
+            python - > gpurun_out/all_workloads.txt <<'PY'
+import glob, json
+for f in sorted(glob.glob("gpurun_out/wl_*.log")):
+    for line in open(f):
+        if line.startswith("{"):
+            d = json.loads(line); r = d.get("roofline") or {}
+            print(f[len("gpurun_out/wl_"):-4], d["value"], r.get("frac"), r.get("kernel_ms_alone"), d.get("decode_check"))
+PY
+            cat gpurun_out/all_workloads.txt ;;
     shardmajor) run pytest_shardmajor 600 python -u -m pytest tests/test_gpu_shardmajor.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     masks)  run pytest_masks 600 python -u -m pytest tests/test_gpu_masks.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     mixed)  for wl in small_mixed encdec_mixed small; do
