@@ -22,7 +22,8 @@ than tests/test_gpu_random.py:
   * round 4: worker objects past max_shard in pinned Split images (column
     slices over several mailboxes, shards up to 64 KiB) and host ops coded in
     column slabs (RSGPU_SLAB_BYTES drawn small, so objects of a few KB take
-    several slabs).
+    several slabs), and pageable objects of 13-20 MB whose staging copies
+    run on the host copy pool.
 Every result is compared bit-exact (bytes) or exactly (booleans, error
 classes) with the oracle on the same input.  Prints a per-kind case count."""
 import collections
@@ -503,6 +504,28 @@ def _objs_case(rng, counts):
                 assert np.array_equal(a, coded[o + i * pitch: o + i * pitch + S]), (tag, op, lost, i)
 
 
+def _large_pageable_case(rng, counts):
+    """a pageable object past the host copy pool's threshold (12 MiB of rows):
+    the staging copies run on the pool (hostcopy.cpp)"""
+    k, p = 10, int(rng.integers(1, 5))
+    n = k + p
+    size = int(rng.integers(1_300_000, 2_000_000))
+    data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)]
+    e, full = oracle.encode(k, p, data + [bytes(size)] * p)
+    assert e == 0
+    enc = ia.New(k, p)
+    sh = [np.frombuffer(bytes(full[i]), np.uint8).copy() if i < k else np.zeros(size, np.uint8) for i in range(n)]
+    assert enc.EncodeVerify(sh)
+    for i in range(k, n):
+        assert np.array_equal(sh[i], np.frombuffer(bytes(full[i]), np.uint8)), ("large", i)
+    lost = sorted(rng.choice(n, p, replace=False).tolist())
+    got = [None if i in lost else sh[i] for i in range(n)]
+    assert enc.DecodeVerify(got)
+    for i in lost:
+        assert np.array_equal(got[i], np.frombuffer(bytes(full[i]), np.uint8)), ("large", lost, i)
+    counts["large_pageable"] += 1
+
+
 def _slab_case(rng, counts):
     """a host op with a small slab size: the object is coded in column slabs"""
     os.environ["RSGPU_SLAB_BYTES"] = str(int(rng.integers(4096, 1 << 16)))
@@ -534,8 +557,10 @@ def test_gpu_soak_vs_oracle(gpu):
             _worker_case(rng, counts)
         elif r < 0.94:
             _objs_case(rng, counts)
-        else:
+        elif r < 0.99:
             _slab_case(rng, counts)
+        else:
+            _large_pageable_case(rng, counts)
         if time.time() - last > 30:  # progress line (a silent GPU run reads as hung)
             last = time.time()
             print(f"soak {last - t0:.0f}s: {sum(counts.values())} cases", flush=True)
