@@ -95,7 +95,9 @@ void copy_rows(const CopyJob *jobs, size_t n) {
     for (size_t i = 0; i < n; ++i) total += jobs[i].len;
     Pool *p = total >= kMinParallel ? pool() : nullptr;
     if (!p || p->nthreads == 0 || !p->busy.try_lock()) {
-        for (size_t i = 0; i < n; ++i) std::memcpy(jobs[i].dst, jobs[i].src, jobs[i].len);
+        // empty rows may carry null pointers (memcpy's arguments must not be)
+        for (size_t i = 0; i < n; ++i)
+            if (jobs[i].len) std::memcpy(jobs[i].dst, jobs[i].src, jobs[i].len);
         return;
     }
     {
