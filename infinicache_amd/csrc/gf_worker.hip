@@ -985,7 +985,7 @@ int worker_run_split(Worker &w, uint32_t op, size_t S, uint32_t mask, const uint
     for (int j = 0; j < m; ++j) {
         const int i = got[j];
         const size_t b0 = (size_t)j * slice, len = std::min(slice, S - b0);
-        uintptr_t pin = (uintptr_t)(img + b0), pout = pin;
+        uintptr_t pin = staged ? 0 : (uintptr_t)(img + b0), pout = pin;
         size_t pitch = S;
         if (staged) {
             uint8_t *dst = w.vram ? w.v_img[i] : w.stage_h[i];

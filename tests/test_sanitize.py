@@ -26,7 +26,7 @@ def _runtime_dir():
 def san_client():
     if not os.path.exists(CLANG):
         pytest.skip("no clang in this image")
-    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "infinicache_amd", "csrc"), "sanitize"])
+    subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "infinicache_amd", "csrc"), "sanitize"])
     out = os.path.join(SAN, "c_abi_client_san")
     rt = _runtime_dir()
     subprocess.check_call([
@@ -61,3 +61,71 @@ def test_c_abi_gpu_paths_under_asan_ubsan(gpu, san_client):
     assert r.returncode == 0, r.stderr[-4000:] + r.stdout
     assert "gpu checks ok" in r.stdout
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+def _stress_client(kind):
+    """tests/c_abi_stress.c built against librsgpu_san.so (kind "asan": ASan +
+    UBSan) or librsgpu_tsan.so ("tsan"), or against the product library
+    (kind "plain")."""
+    if not os.path.exists(CLANG):
+        pytest.skip("no clang in this image")
+    src = [os.path.join(HERE, "c_abi_stress.c"), os.path.join(ROOT, "oracle", "rs_oracle.c")]
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle")]
+    os.makedirs(SAN, exist_ok=True)
+    out = os.path.join(SAN, "c_abi_stress_" + kind)
+    if kind == "plain":
+        lib = os.path.join(ROOT, "infinicache_amd")
+        subprocess.check_call([CLANG, "-O2", "-std=c11", "-D_GNU_SOURCE", *inc, *src, "-o", out, "-L", lib,
+                               "-l:librsgpu.so", "-Wl,-rpath," + lib, "-lpthread"])
+        return out
+    subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "infinicache_amd", "csrc"),
+                           "sanitize" if kind == "asan" else "tsan"])
+    flags = ["-fsanitize=address,undefined", "-shared-libasan"] if kind == "asan" else ["-fsanitize=thread"]
+    lib = "-l:librsgpu_san.so" if kind == "asan" else "-l:librsgpu_tsan.so"
+    subprocess.check_call([CLANG, "-O1", "-g", "-std=c11", "-D_GNU_SOURCE", "-fno-omit-frame-pointer", *flags, *inc,
+                           *src, "-o", out, "-L", SAN, lib, "-Wl,-rpath," + SAN, "-Wl,-rpath," + _runtime_dir(),
+                           "-lpthread"])
+    return out
+
+
+def test_stress_clients_build():
+    """The stress client links against all three libraries (the runs need a GPU)."""
+    for kind in ("plain", "asan", "tsan"):
+        assert os.path.exists(_stress_client(kind))
+
+
+def _stress(kind, threads, seconds, seed):
+    exe = _stress_client(kind)
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1"
+    env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
+    env["TSAN_OPTIONS"] = ("halt_on_error=1:exitcode=66:second_deadlock_stack=1:suppressions="
+                           + os.path.join(HERE, "tsan.supp"))
+    r = subprocess.run([exe, str(threads), str(seconds), str(seed)], capture_output=True, text=True,
+                       timeout=seconds + 60, env=env)
+    print(r.stdout)
+    assert r.returncode == 0, r.stderr[-6000:] + r.stdout
+    assert "all bit-exact" in r.stdout
+    for bad in ("ERROR: AddressSanitizer", "runtime error", "WARNING: ThreadSanitizer"):
+        assert bad not in r.stderr, r.stderr[-6000:]
+    return r.stdout
+
+
+@pytest.mark.gpu
+def test_stress_every_route_concurrently(gpu):
+    """16 threads on one context, the product library: worker (mailbox image,
+    in place, column slices in place and staged), stream path with slot
+    growth, copy pool, pinned images freed per call, all at once."""
+    _stress("plain", 16, 15, 1)
+
+
+@pytest.mark.gpu
+def test_stress_under_asan_ubsan(gpu):
+    _stress("asan", 8, 15, 2)
+
+
+@pytest.mark.gpu
+def test_stress_under_tsan(gpu):
+    """Data races in the host side (slots, worker mailboxes and reader epochs,
+    deferred frees, copy pool) under ThreadSanitizer with the kernels running."""
+    _stress("tsan", 8, 15, 3)
