@@ -82,9 +82,17 @@ def _stress_client(kind):
                            "sanitize" if kind == "asan" else "tsan"])
     flags = ["-fsanitize=address,undefined", "-shared-libasan"] if kind == "asan" else ["-fsanitize=thread"]
     lib = "-l:librsgpu_san.so" if kind == "asan" else "-l:librsgpu_tsan.so"
-    subprocess.check_call([CLANG, "-O1", "-g", "-std=c11", "-D_GNU_SOURCE", "-fno-omit-frame-pointer", *flags, *inc,
-                           *src, "-o", out, "-L", SAN, lib, "-Wl,-rpath," + SAN, "-Wl,-rpath," + _runtime_dir(),
-                           "-lpthread"])
+    objs = []
+    for f in src:
+        o = os.path.join(SAN, kind + "_" + os.path.basename(f) + ".o")
+        subprocess.check_call([CLANG, "-O1", "-g", "-std=c11", "-D_GNU_SOURCE", "-fno-omit-frame-pointer", *flags,
+                               *inc, "-c", f, "-o", o])
+        objs.append(o)
+    # linked by the C++ driver: it exports the runtime's C++ interceptors
+    # (operator new/delete, the __cxa_guard_* of the library's function-local
+    # statics) from the executable, which a C link leaves out
+    subprocess.check_call([CLANG + "++", *flags, *objs, "-o", out, "-L", SAN, lib, "-Wl,-rpath," + SAN,
+                           "-Wl,-rpath," + _runtime_dir(), "-lpthread"])
     return out
 
 
