@@ -124,16 +124,16 @@ def test_stress_every_route_concurrently(gpu):
     """16 threads on one context, the product library: worker (mailbox image,
     in place, column slices in place and staged), stream path with slot
     growth, copy pool, pinned images freed per call, all at once."""
-    _stress("plain", 16, 15, 1)
+    _stress("plain", 16, 10, 1)
 
 
 @pytest.mark.gpu
 def test_stress_under_asan_ubsan(gpu):
-    _stress("asan", 8, 15, 2)
+    _stress("asan", 8, 10, 2)
 
 
 @pytest.mark.gpu
 def test_stress_under_tsan(gpu):
     """Data races in the host side (slots, worker mailboxes and reader epochs,
     deferred frees, copy pool) under ThreadSanitizer with the kernels running."""
-    _stress("tsan", 8, 15, 3)
+    _stress("tsan", 8, 12, 3)
