@@ -318,8 +318,8 @@ int run_host(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     uint32_t bad_all = 0, then_all = 0;
     for (size_t b0 = 0; b0 < size; b0 += L) {
         const size_t l = std::min(L, size - b0);
-        for (size_t i = 0; i < in.size(); ++i) in[i] = in_src[i] + b0;
-        for (size_t i = 0; i < out.size(); ++i) out[i] = out_dst[i] + b0;
+        for (size_t i = 0; i < in.size(); ++i) in[i] = in_src[i] ? in_src[i] + b0 : nullptr;
+        for (size_t i = 0; i < out.size(); ++i) out[i] = out_dst[i] ? out_dst[i] + b0 : nullptr;
         uint32_t b = 0, tb = 0;
         const int e = run_host_once(ctx, plan, nrows_staged, l, in, out, bad ? &b : nullptr, then,
                                     then_bad ? &tb : nullptr);
