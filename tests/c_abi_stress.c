@@ -13,9 +13,11 @@
  * CPU oracle (orc_encode), drop up to `parity` random shards, fused decode
  * (Client.decode, ecRedis.go:404-427), compare every rebuilt row.
  *
- *   c_abi_stress <threads> <seconds> [seed]
+ *   c_abi_stress <threads> <seconds> [seed [data parity]]
  *
- * Routes (RS(10+2), worker on with 16 mailboxes, max_shard 4 KiB):
+ * Routes (RS(10+2) unless given, worker on with 16 mailboxes, max_shard 4 KiB;
+ * object sizes below are for RS(10+2), the shard lengths are the same for
+ * every code):
  *   0  1 KiB object, pageable pointer table     -> worker, mailbox image
  *   1  1 KiB object, pinned Split image         -> worker, in place
  *   2  100 KiB object, pinned Split image       -> worker column slices in place
@@ -38,7 +40,8 @@
 
 int orc_encode(int k, int p, int kind, uint8_t *const *shards, const size_t *lens, int nshards);
 
-enum { K = 10, P = 2, N = 12, ROUTES = 7 };
+enum { MAXN = 16, ROUTES = 7 };
+static int K = 10, P = 2, N = 12; /* the code (argv 4, 5): data + parity <= 16 */
 
 static rsgpu_ctx *ctx;
 static double deadline;
@@ -69,8 +72,8 @@ static uint64_t next(uint64_t *s) {
 
 /* one Client.encode + Client.decode round on the rows rows[0..N) of S bytes */
 static int one_object(int route, size_t S, uint8_t **rows, int image, uint64_t *rng) {
-    size_t lens[N];
-    uint8_t *ref[N];
+    size_t lens[MAXN];
+    uint8_t *ref[MAXN];
     for (int i = 0; i < N; i++) {
         lens[i] = S;
         ref[i] = malloc(S ? S : 1);
@@ -117,7 +120,7 @@ static int one_round(int route, uint64_t *rng, uint8_t **img, size_t *img_cap) {
         case 5: S = (1300u << 10) + (size_t)(next(rng) % (400u << 10)); break;   /* 13-17 MiB */
         default: S = 1 + (size_t)(next(rng) % 4096); break;
     }
-    uint8_t *rows[N];
+    uint8_t *rows[MAXN];
     int rc;
     if (route == 1 || route == 2) {  /* the thread's own pinned image, kept across calls */
         if (*img_cap < N * S) {
@@ -168,6 +171,12 @@ int main(int argc, char **argv) {
     const int threads = argc > 1 ? atoi(argv[1]) : 8;
     const double seconds = argc > 2 ? atof(argv[2]) : 10;
     if (argc > 3) seed0 = strtoull(argv[3], NULL, 10);
+    if (argc > 5) {
+        K = atoi(argv[4]);
+        P = atoi(argv[5]);
+        N = K + P;
+        if (K < 1 || P < 1 || N > MAXN) return fprintf(stderr, "code must have 1 <= data, parity and data+parity <= 16\n"), 2;
+    }
     if (rsgpu_create(K, P, 0, 0, &ctx) != RSGPU_OK) return fprintf(stderr, "create failed\n"), 1;
     if (rsgpu_worker_start(ctx, 16, 0, 0) != RSGPU_OK) return fprintf(stderr, "worker_start failed\n"), 1;
     deadline = now_s() + seconds;
@@ -185,7 +194,7 @@ int main(int argc, char **argv) {
     rsgpu_destroy(ctx);
     long total = 0;
     for (int i = 0; i < ROUTES; i++) total += counts[i];
-    printf("stress: %d threads, %.0f s, %ld objects (routes:", nt, seconds, total);
+    printf("stress: RS(%d+%d), %d threads, %.0f s, %ld objects (routes:", K, P, nt, seconds, total);
     for (int i = 0; i < ROUTES; i++) printf(" %ld", counts[i]);
     printf("), worker served %llu declined %llu launches %llu: %s\n", (unsigned long long)served,
            (unsigned long long)declined, (unsigned long long)launches, bad ? "FAILED" : "all bit-exact");

@@ -102,14 +102,14 @@ def test_stress_clients_build():
         assert os.path.exists(_stress_client(kind))
 
 
-def _stress(kind, threads, seconds, seed):
+def _stress(kind, threads, seconds, seed, code=()):
     exe = _stress_client(kind)
     env = dict(os.environ)
     env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1"
     env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
     env["TSAN_OPTIONS"] = ("halt_on_error=1:exitcode=66:second_deadlock_stack=1:suppressions="
                            + os.path.join(HERE, "tsan.supp"))
-    r = subprocess.run([exe, str(threads), str(seconds), str(seed)], capture_output=True, text=True,
+    r = subprocess.run([exe, str(threads), str(seconds), str(seed), *map(str, code)], capture_output=True, text=True,
                        timeout=seconds + 60, env=env)
     print(r.stdout)
     assert r.returncode == 0, r.stderr[-6000:] + r.stdout
@@ -125,6 +125,14 @@ def test_stress_every_route_concurrently(gpu):
     in place, column slices in place and staged), stream path with slot
     growth, copy pool, pinned images freed per call, all at once."""
     _stress("plain", 16, 10, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("code", [(4, 2), (12, 4), (1, 1)])
+def test_stress_other_codes(gpu, code):
+    """The same routes on other codes: RS(12+4) (four rows per worker pass),
+    RS(4+2), and RS(1+1)."""
+    _stress("plain", 8, 5, 40 + code[0], code)
 
 
 @pytest.mark.gpu
