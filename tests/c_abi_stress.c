@@ -13,7 +13,7 @@
  * CPU oracle (orc_encode), drop up to `parity` random shards, fused decode
  * (Client.decode, ecRedis.go:404-427), compare every rebuilt row.
  *
- *   c_abi_stress <threads> <seconds> [seed [data parity]]
+ *   c_abi_stress <threads> <seconds> [seed [data parity [matrix kind]]]
  *
  * Routes (RS(10+2) unless given, worker on with 16 mailboxes, max_shard 4 KiB;
  * object sizes below are for RS(10+2), the shard lengths are the same for
@@ -42,6 +42,7 @@ int orc_encode(int k, int p, int kind, uint8_t *const *shards, const size_t *len
 
 enum { MAXN = 16, ROUTES = 7 };
 static int K = 10, P = 2, N = 12; /* the code (argv 4, 5): data + parity <= 16 */
+static unsigned KIND = RSGPU_MATRIX_VANDERMONDE; /* argv 6: 0 Vandermonde, 1 Cauchy */
 
 static rsgpu_ctx *ctx;
 static double deadline;
@@ -90,7 +91,7 @@ static int one_object(int route, size_t S, uint8_t **rows, int image, uint64_t *
     int ok = 7, rc;
     rc = image ? rsgpu_encode_verify_image(ctx, rows[0], S, N, &ok) : rsgpu_encode_verify(ctx, rows, lens, N, &ok);
     if (rc != RSGPU_OK || ok != 1) FAIL("encode_verify rc=%d ok=%d", rc, ok);
-    if (orc_encode(K, P, 0, ref, lens, N)) FAIL("oracle");
+    if (orc_encode(K, P, (int)KIND, ref, lens, N)) FAIL("oracle");
     for (int i = K; i < N; i++)
         if (memcmp(rows[i], ref[i], S)) FAIL("parity row %d differs from the oracle", i);
     /* drop up to P shards, scribble over them, decode */
@@ -177,7 +178,10 @@ int main(int argc, char **argv) {
         N = K + P;
         if (K < 1 || P < 1 || N > MAXN) return fprintf(stderr, "code must have 1 <= data, parity and data+parity <= 16\n"), 2;
     }
-    if (rsgpu_create(K, P, 0, 0, &ctx) != RSGPU_OK) return fprintf(stderr, "create failed\n"), 1;
+    /* PAR1 is not MDS (some erasure patterns are singular): not a stress kind */
+    if (argc > 6) KIND = (unsigned)atoi(argv[6]);
+    if (KIND > RSGPU_MATRIX_CAUCHY) return fprintf(stderr, "matrix kind must be 0 or 1\n"), 2;
+    if (rsgpu_create(K, P, 0, KIND, &ctx) != RSGPU_OK) return fprintf(stderr, "create failed\n"), 1;
     if (rsgpu_worker_start(ctx, 16, 0, 0) != RSGPU_OK) return fprintf(stderr, "worker_start failed\n"), 1;
     deadline = now_s() + seconds;
     pthread_t th[64];
@@ -194,7 +198,8 @@ int main(int argc, char **argv) {
     rsgpu_destroy(ctx);
     long total = 0;
     for (int i = 0; i < ROUTES; i++) total += counts[i];
-    printf("stress: RS(%d+%d), %d threads, %.0f s, %ld objects (routes:", K, P, nt, seconds, total);
+    printf("stress: RS(%d+%d)%s, %d threads, %.0f s, %ld objects (routes:", K, P, KIND ? " Cauchy" : "", nt, seconds,
+           total);
     for (int i = 0; i < ROUTES; i++) printf(" %ld", counts[i]);
     printf("), worker served %llu declined %llu launches %llu: %s\n", (unsigned long long)served,
            (unsigned long long)declined, (unsigned long long)launches, bad ? "FAILED" : "all bit-exact");

@@ -128,10 +128,10 @@ def test_stress_every_route_concurrently(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("code", [(4, 2), (12, 4), (1, 1)])
+@pytest.mark.parametrize("code", [(4, 2, 0), (12, 4, 0), (1, 1, 0), (10, 4, 1)])
 def test_stress_other_codes(gpu, code):
     """The same routes on other codes: RS(12+4) (four rows per worker pass),
-    RS(4+2), and RS(1+1)."""
+    RS(4+2), RS(1+1), and RS(10+4) on upstream's Cauchy matrix."""
     _stress("plain", 8, 5, 40 + code[0], code)
 
 
