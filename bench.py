@@ -9,11 +9,20 @@ rows <- M x data rows, Client.encode / ecRedis.go:390) then decode it
 Client.decode / ecRedis.go:406-420 with the proxy's first-d rule: exactly k
 shards arrive).  Each rank owns its own batch of 1024 objects (object-per-
 rank, weak scaling); RCCL all_reduce of one int is the start/finish barrier.
-value = object bytes x ops of all ranks / max-over-ranks time.
+value = object bytes x ops of all ranks / max-over-ranks time.  At N > 1 (or
+with --collectives) the same line carries a `strong_scaling` block: the
+workload's one batch split over the ranks (shard_objects), timed after the
+weak region with the same barriers.
 
-Prints ONE JSON line (rank 0) with roofline (HIP-event kernel timing, the
-committed rocprofv3 PMC traffic when available) and cpu_baseline (the
-oracle's AVX2 port of the Go path, timed on this host, rank 0, N=1 only).
+Prints ONE JSON line (rank 0) with roofline (HIP-event kernel timing;
+`traffic` measured in this run by two rocprofv3 --pmc child passes at N = 1,
+else the committed summary, `traffic_source` says which) and cpu_baseline
+(the oracle's AVX-512/AVX2 port of the Go path, timed on this host by rank 0
+at every world size, after the timed region).
+
+--collectives (or BENCH_COLLECTIVES=1) issues the collectives at world size 1
+too: under `torch.distributed.run --nproc-per-node 1` that is one RCCL rank
+running the barrier, MAX-reduce and gather of the multi-GPU path.
 """
 from __future__ import annotations
 
@@ -248,46 +257,55 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
 class DistCtx:
     """The only cross-rank traffic of the path: an all_reduce of one int as
     the start/finish barrier (RCCL over xGMI on GPUs, gloo on CPU) and one
-    MAX-reduce of the elapsed time.  Objects never cross ranks."""
+    MAX-reduce of the elapsed time.  Objects never cross ranks.
 
-    def __init__(self, world, rank, device):
+    force: issue the collectives at world size 1 as well (a process group
+    of one rank must exist), so the RCCL path runs on a one-GPU box."""
+
+    def __init__(self, world, rank, device, force=False):
         self.world, self.rank, self.device = world, rank, device
+        self.on = world > 1 or force
+        self.calls = 0  # collectives issued (the 1-rank RCCL test checks them)
 
     def barrier(self):
-        if self.world > 1:
+        if self.on:
             import torch
             import torch.distributed as dist
             t = torch.ones(1, dtype=torch.int32, device=self.device)
             dist.all_reduce(t)
+            self.calls += 1
 
     def max(self, x: float) -> float:
-        if self.world == 1:
+        if not self.on:
             return x
         import torch
         import torch.distributed as dist
         t = torch.tensor([x], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        self.calls += 1
         return float(t.item())
 
     def sum(self, x: int) -> int:
-        if self.world == 1:
+        if not self.on:
             return x
         import torch
         import torch.distributed as dist
         t = torch.tensor([x], dtype=torch.int64, device=self.device)
         dist.all_reduce(t)
+        self.calls += 1
         return int(t.item())
 
     def gather(self, x: float) -> list:
         """Every rank's value of x, in rank order (a SUM-reduce of one-hot
         vectors: the same collective as the barrier, no payload besides)."""
-        if self.world == 1:
+        if not self.on:
             return [x]
         import torch
         import torch.distributed as dist
         t = torch.zeros(self.world, dtype=torch.float64, device=self.device)
         t[self.rank] = x
         dist.all_reduce(t)
+        self.calls += 1
         return [float(v) for v in t.cpu()]
 
 
@@ -368,27 +386,31 @@ def pmc_traffic_live(args, kernel_key, alg_bytes):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from pmc_traffic import per_kernel, short
     key = short(kernel_key)
+    # the children are plain one-process runs: no process group of their own
+    child_env = {kk: v for kk, v in os.environ.items() if kk != "BENCH_COLLECTIVES"}
+    child_env["BENCH_PMC_CHILD"] = "1"
     got = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        out = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [exe, "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv", "--",
-               sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--no-cpu", "--no-pmc",
-               "--steps", "3", "--warmup", "3", "--copies", str(args.copies)]
-        if args.batch:
-            cmd += ["--batch", str(args.batch)]
-        p = subprocess.Popen(cmd, env=dict(os.environ, BENCH_PMC_CHILD="1"), stdout=subprocess.DEVNULL,
-                             stderr=subprocess.DEVNULL, start_new_session=True)
-        try:
-            rc = p.wait(timeout=90)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)  # a refused counter set hangs past SIGTERM
-            p.wait()
-            return None, f"rocprofv3 --pmc {counter} pass timed out (90 s)"
-        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
-        if rc != 0 or not files:
-            return None, f"rocprofv3 --pmc {counter} pass failed (rc {rc})"
-        val = per_kernel(files[0], counter).get(key)
-        shutil.rmtree(out, ignore_errors=True)
+        # the pass's output directory goes whatever happens to the pass (its
+        # counter CSVs can be large)
+        with tempfile.TemporaryDirectory(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp")) as out:
+            cmd = [exe, "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--no-cpu",
+                   "--no-pmc", "--steps", "3", "--warmup", "3", "--copies", str(args.copies)]
+            if args.batch:
+                cmd += ["--batch", str(args.batch)]
+            p = subprocess.Popen(cmd, env=child_env, stdout=subprocess.DEVNULL,
+                                 stderr=subprocess.DEVNULL, start_new_session=True)
+            try:
+                rc = p.wait(timeout=90)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)  # a refused counter set hangs past SIGTERM
+                p.wait()
+                return None, f"rocprofv3 --pmc {counter} pass timed out (90 s)"
+            files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+            if rc != 0 or not files:
+                return None, f"rocprofv3 --pmc {counter} pass failed (rc {rc})"
+            val = per_kernel(files[0], counter).get(key)
         if not val:
             return None, f"rocprofv3 --pmc {counter}: no dispatch of {key}"
         got[counter] = val
@@ -651,6 +673,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="objects per GPU (default: workload's)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the workload's batch is the TOTAL, split over ranks")
+    ap.add_argument("--collectives", action="store_true",
+                    help="issue the barrier / MAX / gather collectives at world size 1 too (one RCCL "
+                         "rank under torch.distributed.run; also BENCH_COLLECTIVES=1)")
     ap.add_argument("--copies", type=int, default=3,
                     help="distinct batches per GPU, step i codes batch i %% copies (cold Infinity Cache)")
     ap.add_argument("--warm", action="store_true",
@@ -690,7 +715,10 @@ def main():
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if os.environ.get("BENCH_SHARE_GPU") == "1":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    force_coll = args.collectives or os.environ.get("BENCH_COLLECTIVES") == "1"
+    dist_on = world > 1 or force_coll
+    if dist_on:
+        os.environ.setdefault("MASTER_PORT", "29517")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -706,7 +734,8 @@ def main():
     w = WORKLOADS[args.workload]
     k, p = w["k"], w["p"]
     n = k + p
-    nobj = args.batch or w["batch"]
+    batch_total = args.batch or w["batch"]
+    nobj = batch_total
     if args.strong:
         nobj = shard_objects(nobj, rank, world)[1]
     S = (w["nbytes"] + k - 1) // k
@@ -759,19 +788,22 @@ def main():
         masks_np = (pres_m.astype(np.int64) << np.arange(n)).sum(axis=1).astype(np.int32)
         masks_dev = torch.from_numpy(masks_np).to(dev)
 
-    def op_encode(buf):
-        enc.encode_dev(buf, S, pitch, stride, nobj, stream)
+    # each op codes the first `cnt` objects of a batch (default: all of them;
+    # the strong-scaling block codes this rank's share of one batch)
+    def op_encode(buf, cnt=None):
+        enc.encode_dev(buf, S, pitch, stride, nobj if cnt is None else cnt, stream)
 
-    def op_decode(buf):
+    def op_decode(buf, cnt=None):
+        c = nobj if cnt is None else cnt
         if w.get("upstream_get"):
-            enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=False, stream=stream)
-            enc.verify_dev(buf, S, pitch, stride, nobj, bad, stream)
+            enc.reconstruct_dev(buf, present, S, pitch, stride, c, data_only=False, stream=stream)
+            enc.verify_dev(buf, S, pitch, stride, c, bad, stream)
         elif w.get("mixed"):
-            enc.decode_dev_masks(buf, masks_dev, S, pitch, stride, nobj, bad, stream)
+            enc.decode_dev_masks(buf, masks_dev, S, pitch, stride, c, bad, stream)
         elif w.get("data_only"):
-            enc.reconstruct_dev(buf, present, S, pitch, stride, nobj, data_only=True, stream=stream)
+            enc.reconstruct_dev(buf, present, S, pitch, stride, c, data_only=True, stream=stream)
         else:
-            enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, stream)
+            enc.decode_dev(buf, present, S, pitch, stride, c, bad, stream)
 
     op_fns = {"encode": op_encode, "decode": op_decode}
 
@@ -850,11 +882,45 @@ def main():
             out[op] = e0.elapsed_time(e1) / args.steps
         return out
 
-    dctx = DistCtx(world, rank, dev)
+    dctx = DistCtx(world, rank, dev, force=force_coll)
     elapsed = timed_run(lambda i: step(), args.steps, args.warmup, lambda: torch.cuda.synchronize(dev), dctx)
     objs_all = dctx.sum(nobj)
     if int(bad.sum()) != 0:
         raise SystemExit("decode reported a verify mismatch on synthetic data")
+
+    # Strong scaling beside the weak line ("strong
+    # scaling of 1024 total"): the workload's ONE batch split over the ranks
+    # by shard_objects, each rank coding its share (a prefix of its own
+    # batches, same rotation) under the same barriers and MAX-over-ranks
+    # timing.  Timed after the weak region; not the line's `value`.
+    strong = None
+    if dist_on and not args.strong:
+        s_start, s_cnt = shard_objects(batch_total, rank, world)
+        sturn = [0]
+
+        def sstep(i):
+            buf = bufs[sturn[0] % copies]
+            sturn[0] += 1
+            for op in w["ops"]:
+                op_fns[op](buf, s_cnt)
+
+        s_el = timed_run(sstep, args.steps, max(3, args.warmup // 10), lambda: torch.cuda.synchronize(dev), dctx)
+        if int(bad.sum()) != 0:
+            raise SystemExit("decode reported a verify mismatch on synthetic data (strong block)")
+        s_objs = dctx.sum(s_cnt)
+        s_counts = [int(round(c)) for c in dctx.gather(float(s_cnt))]
+        strong = {
+            "value": round(s_objs * w["nbytes"] * len(w["ops"]) * args.steps / s_el / GiB, 2),
+            "unit": "GiB/s",
+            "ms_per_step": round(s_el / args.steps * 1e3, 4),
+            "batch_total": batch_total,
+            "objects_coded": s_objs,
+            "objects_per_rank": s_counts,
+            "note": "the workload's one batch split over the ranks (shard_objects), max-over-ranks time, "
+                    "same barriers; timed after the weak region, not the line's value",
+        }
+        if s_objs != batch_total:
+            raise SystemExit(f"strong block coded {s_objs} objects, batch is {batch_total}")
     # Untimed proof that the timed ops did their work: on batch 0, overwrite
     # every row an op writes (encode: the parity rows; decode: each object's
     # erased rows) with random garbage, run the op, and compare the rows'
@@ -1014,7 +1080,7 @@ def main():
                 "batch_copies": copies,
                 "decode_erasures": list(w["lost"]),
                 "parallelism": (f"object-per-rank x{world} "
-                                + ("(one process, no collective)" if world == 1 else
+                                + ("(one process, no collective)" if not dist_on else
                                    f"({'RCCL' if backend == 'nccl' else backend} all_reduce barrier only"
                                    + (", ranks sharing one GPU)" if os.environ.get("BENCH_SHARE_GPU") == "1"
                                       else ")"))),
@@ -1023,10 +1089,12 @@ def main():
             **({"decode_check": work_check["decode"]["result"]} if "decode" in work_check else {}),
             "work_check": work_check,
             **({"warm_repeat": warm} if warm else {}),
+            **({"strong_scaling": strong} if strong else {}),
+            **({"collectives_issued": dctx.calls} if dist_on else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -373,13 +373,26 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
 int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *present,
                        const size_t *shard_lens, int nobj, int *ok);
 
-/* Pinned host memory helpers (hipHostRegister / hipHostMalloc).  free and
- * unregister park any resident worker around the runtime call (it would
- * otherwise wait for the worker to idle out). */
+/* Pinned host memory helpers (hipHostRegister / hipHostMalloc; alloc takes
+ * Mapped | Coherent pages, RSGPU_HOST_ALLOC=default the runtime's default
+ * kind).  hipHostFree / hipHostUnregister wait for every kernel of the
+ * device, a resident worker's too: with no worker kernel resident they run at
+ * once; otherwise unregister parks the workers around the call and free is
+ * deferred to the next moment no worker kernel is resident (at most 256 MiB
+ * held; past that it parks the workers too). */
 int rsgpu_host_register(void *p, size_t len);
 int rsgpu_host_unregister(void *p);
 int rsgpu_host_alloc(size_t len, void **out);
 int rsgpu_host_free(void *p);
+
+/* ---- diagnostics and test knobs ------------------------------------------
+ * Library buffers whose free is being held back because a worker kernel is
+ * resident (count, bytes) and the number of frees ever held back. */
+int rsgpu_retired_stats(size_t *count, size_t *bytes, uint64_t *deferred);
+/* Staged bytes per object above which the per-object host calls code in
+ * column slabs (default 1 GiB; RSGPU_SLAB_BYTES at first use).  bytes < 4096
+ * restores the default.  Process-wide; set it while no call is in flight. */
+int rsgpu_set_slab_bytes(size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -5,12 +5,13 @@ from .ec import (ALL_DEVICES, DummyEncoder, ErrInvalidInput, ErrInvShardNum, Err
                  ErrNotImplemented, ErrReconstructRequired, ErrShardNoData, ErrShardSize,
                  ErrShortData, ErrSingular, ErrTooFewShards, HipError, InvalidArgument, New,
                  NewEncoder, NoDevice, RSEncoder, RSError, device_count, device_ok, host_alloc,
-                 host_register, host_unregister, shardmajor_layout)
+                 host_register, host_unregister, retired_stats, set_slab_bytes, shardmajor_layout)
 
 __all__ = [
     "New", "NewEncoder", "RSEncoder", "DummyEncoder", "RSError", "device_count", "device_ok",
     "ErrInvShardNum", "ErrMaxShardNum", "ErrTooFewShards", "ErrShardNoData", "ErrShardSize",
     "ErrSingular", "ErrShortData", "ErrReconstructRequired", "ErrInvalidInput",
     "ErrNotImplemented", "InvalidArgument", "NoDevice", "HipError", "host_alloc",
-    "host_register", "host_unregister", "shardmajor_layout", "ALL_DEVICES",
+    "host_register", "host_unregister", "shardmajor_layout", "ALL_DEVICES", "retired_stats",
+    "set_slab_bytes",
 ]

@@ -27,7 +27,7 @@ EXPORTS = (
     "rsgpu_verify_image", "rsgpu_reconstruct_image", "rsgpu_decode_image", "rsgpu_device_calls",
     "rsgpu_encode_dev_objs", "rsgpu_verify_dev_objs", "rsgpu_reconstruct_dev_objs", "rsgpu_decode_dev_objs",
     "rsgpu_worker_start", "rsgpu_worker_stop", "rsgpu_worker_stats", "rsgpu_shardmajor_layout",
-    "rsgpu_copy_pieces",
+    "rsgpu_copy_pieces", "rsgpu_retired_stats", "rsgpu_set_slab_bytes",
 )
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -118,5 +118,7 @@ def load():
     L.rsgpu_host_unregister.argtypes = [vp]
     L.rsgpu_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
     L.rsgpu_host_free.argtypes = [vp]
+    L.rsgpu_retired_stats.argtypes = [szp, szp, u64p]
+    L.rsgpu_set_slab_bytes.argtypes = [sz]
     _lib = L
     return L

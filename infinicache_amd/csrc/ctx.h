@@ -34,10 +34,10 @@ struct Slot {
     uint32_t *m_bad = nullptr;  // device address of h_bad (mapped pinned memory)
     ~Slot() {
         if (stream) (void)hipStreamDestroy(stream);
-        retire(h, true);
-        retire(d, false);
-        retire(d_bad, false);
-        retire(h_bad, true);
+        retire(h, true, cap);
+        retire(d, false, cap);
+        retire(d_bad, false, 4);
+        retire(h_bad, true, 4);
     }
 };
 
@@ -45,11 +45,32 @@ inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Staged image bytes (rows x shard length) above which the host calls code
 // one object in column slabs (rsgpu.cpp run_host; the batch pipelines hand
-// such objects to it).  RSGPU_SLAB_BYTES overrides it, for tests.
-inline size_t slab_bytes() {
-    const char *v = std::getenv("RSGPU_SLAB_BYTES");
-    const long long b = v ? std::atoll(v) : 0;
-    return b >= 4096 ? (size_t)b : ((size_t)1 << 30);
+// such objects to it).  Read once: RSGPU_SLAB_BYTES at the first call, or
+// rsgpu_set_slab_bytes (tests) — no getenv on the call path (a
+// per-call getenv raced with setenv from other threads).
+constexpr size_t kSlabDefault = (size_t)1 << 30;
+inline std::atomic<size_t> &slab_setting() {
+    static std::atomic<size_t> v{[] {
+        const char *e = std::getenv("RSGPU_SLAB_BYTES");
+        const long long b = e ? std::atoll(e) : 0;
+        return b >= 4096 ? (size_t)b : kSlabDefault;
+    }()};
+    return v;
+}
+inline size_t slab_bytes() { return slab_setting().load(std::memory_order_relaxed); }
+
+// Pinned host memory that kernels read and write in place over PCIe (the
+// Split images of rsgpu_host_alloc, the stream path's staging images):
+// Mapped | Coherent, the kind the resident worker's mailboxes always used.
+// hipHostMallocDefault — the kind the round-3 probe faulted on
+// — only with RSGPU_HOST_ALLOC=default (read once).
+inline unsigned host_image_flags() {
+    static const unsigned f = [] {
+        const char *e = std::getenv("RSGPU_HOST_ALLOC");
+        return e && std::strcmp(e, "default") == 0 ? (unsigned)hipHostMallocDefault
+                                                   : (unsigned)(hipHostMallocMapped | hipHostMallocCoherent);
+    }();
+    return f;
 }
 
 inline bool debug_on() {
@@ -89,8 +110,8 @@ struct PipeSlot {
     uint32_t *d_bad = nullptr;
     ~PipeSlot() {
         if (stream) (void)hipStreamDestroy(stream);
-        retire(d, false);
-        retire(d_bad, false);
+        retire(d, false, cap);
+        retire(d_bad, false, 4);
     }
 };
 
@@ -399,14 +420,15 @@ struct rsgpu_ctx {
         if (s->cap < bytes) {
             // the old images are retired (freed at once unless a worker runs);
             // growth at least 1.5x bounds what a running worker keeps
-            retire(s->h, true);
-            retire(s->d, false);
+            retire(s->h, true, s->cap);
+            retire(s->d, false, s->cap);
             const size_t cap = round_up(std::max(bytes, s->cap + s->cap / 2), (size_t)1 << 20);
             s->h = nullptr; s->d = nullptr; s->hdev = nullptr; s->cap = 0;
-            HIP_TRY(hipHostMalloc(&s->h, cap, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc(&s->h, cap, host_image_flags()));
             HIP_TRY(hipHostGetDevicePointer((void **)&s->hdev, s->h, 0));
             HIP_TRY(hipMalloc(&s->d, cap));
             s->cap = cap;
+            relieve_retired();  // (no lock held here) the kept bytes stay bounded
         }
         return RSGPU_OK;
     }

@@ -999,8 +999,8 @@ MultiWorkspace::~MultiWorkspace() {
     if (upload) (void)hipStreamDestroy(upload);
     for (auto &s : slot) {
         if (s.done) (void)hipEventDestroy(s.done);
-        retire(s.d, false);
-        retire(s.h, true);
+        retire(s.d, false, s.cap);
+        retire(s.h, true, s.cap);
     }
 }
 
@@ -1089,8 +1089,8 @@ hipError_t stage_image(MultiWorkspace &ws, const std::vector<uint8_t> &img, Mult
         if (e != hipSuccess) return e;
     }
     if (w.cap < img.size()) {
-        retire(w.d, false);  // (freed once no worker runs: devmem.cpp)
-        retire(w.h, true);
+        retire(w.d, false, w.cap);  // (held while a worker kernel is resident: devmem.cpp)
+        retire(w.h, true, w.cap);
         w.d = nullptr;
         w.h = nullptr;
         w.cap = 0;

@@ -763,7 +763,10 @@ int wait_for(Worker &w, int i, const uint32_t (&rq)[8], const uint32_t n, uint32
                 // every workgroup of `cur` leaves promptly
                 hipError_t he = hipStreamSynchronize(w.stream);
                 if (he != hipSuccess) return fail(hip_fail(he, "resident worker"));
-                if ((he = launch(w, cur + 1)) != hipSuccess) return fail(hip_fail(he, "resident worker launch"));
+                // serialised with the library's frees (devmem.cpp), which
+                // also go now if no other worker kernel is resident
+                he = launch_guarded([&] { return launch(w, cur + 1); });
+                if (he != hipSuccess) return fail(hip_fail(he, "resident worker launch"));
                 w.gen.store(cur + 1, std::memory_order_release);
                 w.launches.fetch_add(1, std::memory_order_relaxed);
             }
@@ -857,6 +860,8 @@ std::set<rsgpu_ctx *> g_live;
 // workers it touches; two of them interleaving would each hold a part)
 std::mutex g_park_mu;
 
+bool workers_resident();  // below (devmem.cpp's probe)
+
 void stop_all_workers() {
     std::vector<rsgpu_ctx *> live;
     {
@@ -867,7 +872,10 @@ void stop_all_workers() {
 }
 void track_worker(rsgpu_ctx *ctx, bool on) {
     static std::once_flag once;
-    std::call_once(once, [] { std::atexit(stop_all_workers); });
+    std::call_once(once, [] {
+        std::atexit(stop_all_workers);
+        set_resident_probe(workers_resident);
+    });
     std::lock_guard<std::mutex> l(g_live_mu);
     if (on) g_live.insert(ctx);
     else g_live.erase(ctx);
@@ -895,6 +903,19 @@ struct WorkerRef {
     WorkerRef(const WorkerRef &) = delete;
     WorkerRef &operator=(const WorkerRef &) = delete;
 };
+
+// devmem.cpp's probe (called with its lock held): some started worker's
+// kernel is launched and not finished.  Each worker is read inside a reader
+// epoch, so a concurrent stop cannot free it meanwhile (and this never drops
+// the last reference).
+bool workers_resident() {
+    std::lock_guard<std::mutex> l(g_live_mu);
+    for (rsgpu_ctx *c : g_live) {
+        const WorkerRef ref(c);
+        if (ref.w && hipStreamQuery(ref.w->stream) == hipErrorNotReady) return true;
+    }
+    return false;
+}
 
 // ctx's worker stopped and detached (ctx->worker_mu and g_park_mu held)
 int stop_locked(rsgpu_ctx *ctx) {

@@ -110,16 +110,30 @@ int rsgpu_copy_pieces(rsgpu_ctx *ctx, const void *d_src, size_t src_pitch, size_
     if (shard_len == 0) return RSGPU_ERR_SHARD_NO_DATA;
     if (ctx->n < 64 && (rows >> ctx->n) != 0) return RSGPU_ERR_INVALID_ARG;
     // pieces of one layout never overlap: src_obj_stride / dst_obj_stride >=
-    // shard_len when nobj > 1 (row pitches are checked by the spans below)
+    // shard_len when nobj > 1
     if (nobj > 1 && (src_obj_stride < shard_len || dst_obj_stride < shard_len)) return RSGPU_ERR_INVALID_ARG;
+    std::vector<uint32_t> list;
+    for (int i = 0; i < ctx->n && i < 64; ++i)
+        if ((rows >> i) & 1) list.push_back((uint32_t)i);
+    const size_t maxrow = list.empty() ? 0 : list.back();
+    // ... and neither do its rows (check_layout's rule, over the rows that
+    // move): object-major, each object's rows 0..maxrow inside its stride;
+    // shard-major, each row holding every object's piece.  Workgroups write
+    // pieces concurrently, so an overlapping destination would be silent,
+    // nondeterministic corruption; a malformed source is refused
+    // the same way.
+    auto layout_ok = [&](size_t pitch, size_t stride) {
+        if (list.size() > 1 && pitch < shard_len) return false;
+        if (nobj > 1 && list.size() > 0 && stride < (maxrow + 1) * pitch &&
+            !(stride >= shard_len && pitch >= (size_t)(nobj - 1) * stride + shard_len))
+            return false;
+        return true;
+    };
+    if (!layout_ok(src_pitch, src_obj_stride) || !layout_ok(dst_pitch, dst_obj_stride)) return RSGPU_ERR_INVALID_ARG;
     DeviceGuard dg_;
     int e = ctx->use_device(dg_);
     if (e) return e;
     if (nobj == 0 || rows == 0) return RSGPU_OK;
-    std::vector<uint32_t> list;
-    for (int i = 0; i < ctx->n && i < 64; ++i)
-        if ((rows >> i) & 1) list.push_back((uint32_t)i);
-    const size_t maxrow = list.back();
     if (maxrow * std::max(src_pitch, dst_pitch) >= ((size_t)1 << 32)) return RSGPU_ERR_INVALID_ARG;
     PieceArgs a{};
     a.src_pitch = (uint32_t)src_pitch;

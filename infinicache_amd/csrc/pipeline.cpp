@@ -58,12 +58,13 @@ int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
     for (auto &s : P.slots) {
         if (s->cap >= bytes) continue;
         HIP_TRY(hipStreamSynchronize(s->stream));
-        retire(s->d, false);  // (freed once no worker runs: devmem.cpp)
+        retire(s->d, false, s->cap);  // (held while a worker kernel is resident: devmem.cpp)
         const size_t cap = round_up(std::max(bytes, s->cap + s->cap / 2), (size_t)1 << 20);
         s->d = nullptr;
         s->cap = 0;
         HIP_TRY(hipMalloc(&s->d, cap));
         s->cap = cap;
+        relieve_retired();  // the kept bytes stay bounded (devmem.cpp)
     }
     return RSGPU_OK;
 }
@@ -71,7 +72,7 @@ int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
 int ensure_flags(rsgpu_ctx *ctx, int nobj) {
     auto &P = ctx->pipe;
     if (P.h_bad_cap >= (size_t)nobj) return RSGPU_OK;
-    retire(P.h_bad, true);
+    retire(P.h_bad, true, P.h_bad_cap * 4);
     const size_t cap = std::max<size_t>({(size_t)nobj, 1, P.h_bad_cap * 2});
     P.h_bad = nullptr;
     P.h_bad_cap = 0;
@@ -152,14 +153,18 @@ int rsgpu_host_register(void *p, size_t len) {
 }
 
 // hipHostUnregister / hipHostFree synchronise the device
-// (profiles/r04_sync_probe*.txt): with a resident worker they would wait
-// until it idles out, so every worker is parked around them
-// (with_workers_parked: calls in flight finish, later ones take the stream
-// path, the next one relaunches).
+// (profiles/r04_sync_probe*.txt): with a resident worker kernel they would
+// wait until it idles out.  With no worker kernel resident they run at once
+// (devmem.cpp holds off relaunches meanwhile); otherwise an unregister parks
+// every worker around it (with_workers_parked: calls in flight finish, later
+// ones take the stream path, the next one relaunches) and a free is deferred
+// to the next moment no kernel is resident, up to kUserKeptCap bytes kept,
+// past which it parks the workers too (a Go stagePool that frees
+// on put no longer parks the workers on every free).
 int rsgpu_host_unregister(void *p) {
     if (!p) return RSGPU_ERR_INVALID_ARG;
     pin_del(p);
-    return with_workers_parked([p] {
+    return device_sync_call([p] {
         HIP_TRY(hipHostUnregister(p));
         return RSGPU_OK;
     });
@@ -171,25 +176,22 @@ int rsgpu_host_alloc(size_t len, void **out) {
     if (rsgpu_device_count() == 0) return RSGPU_ERR_NO_DEVICE;
     // 64 B of slack past the caller's length: kernels may read a Split buffer
     // in place, and a row's last 16-B vector can run past the buffer's end.
-    // Flags: RSGPU_HOST_ALLOC=coherent takes the worker's own kind
-    // (Mapped | Coherent) for a measurement
-    static const unsigned flags = [] {
-        const char *e = std::getenv("RSGPU_HOST_ALLOC");
-        return e && std::strcmp(e, "coherent") == 0 ? (unsigned)(hipHostMallocMapped | hipHostMallocCoherent)
-                                                    : (unsigned)hipHostMallocDefault;
-    }();
-    HIP_TRY(hipHostMalloc(out, len + 64, flags));
+    // Mapped | Coherent (host_image_flags, ctx.h; RSGPU_HOST_ALLOC=default
+    // takes hipHostMallocDefault)
+    HIP_TRY(hipHostMalloc(out, len + 64, host_image_flags()));
     pin_add(*out, len, len + 64);
+    return RSGPU_OK;
+}
+
+int rsgpu_set_slab_bytes(size_t bytes) {
+    slab_setting().store(bytes >= 4096 ? bytes : kSlabDefault, std::memory_order_relaxed);
     return RSGPU_OK;
 }
 
 int rsgpu_host_free(void *p) {
     if (!p) return RSGPU_OK;
     pin_del(p);
-    return with_workers_parked([p] {
-        HIP_TRY(hipHostFree(p));
-        return RSGPU_OK;
-    });
+    return free_user(p, true);
 }
 
 }  // extern "C"

@@ -781,6 +781,7 @@ void rsgpu_destroy(rsgpu_ctx *ctx) {
         hipSetDevice(ctx->device) == hipSuccess)
         g.prev = cur;
     delete ctx;
+    relieve_retired();  // what a resident worker held back stays bounded (devmem.cpp)
 }
 
 int rsgpu_data_shards(const rsgpu_ctx *ctx) { return ctx ? ctx->k : RSGPU_ERR_INVALID_ARG; }
@@ -1184,8 +1185,8 @@ static int recon_dev_multi_atlas(rsgpu_ctx *ctx, void *d_base, const uint8_t *pr
     else HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     const size_t bytes = (size_t)nobj * 4;
     if (w.cap < bytes) {
-        retire(w.d, false);  // (freed once no worker runs: devmem.cpp)
-        retire(w.h, true);
+        retire(w.d, false, w.cap);  // (held while a worker kernel is resident: devmem.cpp)
+        retire(w.h, true, w.cap);
         w.d = nullptr;
         w.h = nullptr;
         w.cap = 0;

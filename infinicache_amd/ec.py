@@ -531,6 +531,21 @@ def host_unregister(arr: np.ndarray) -> None:
     _check(_lib.load().rsgpu_host_unregister(arr.ctypes.data))
 
 
+def retired_stats() -> dict:
+    """rsgpu_retired_stats: library buffers whose free is held back because a
+    worker kernel is resident (count, bytes) and frees ever held back."""
+    L = _lib.load()
+    c, b, d = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_uint64()
+    _check(L.rsgpu_retired_stats(ctypes.byref(c), ctypes.byref(b), ctypes.byref(d)))
+    return {"count": c.value, "bytes": b.value, "deferred": d.value}
+
+
+def set_slab_bytes(nbytes: int) -> None:
+    """rsgpu_set_slab_bytes: staged bytes per object above which host calls
+    code in column slabs (< 4096: the 1 GiB default).  A test knob."""
+    _check(_lib.load().rsgpu_set_slab_bytes(int(nbytes)))
+
+
 def _join(k: int, dst, shards: Sequence, outSize: int) -> None:
     """upstream Join (identical logic in /root/reference/client/ec.go:83-121)."""
     if len(shards) < k:

@@ -258,6 +258,23 @@ def test_copy_pieces_argument_checks():
         enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 64, 100, 4)
     with pytest.raises(ia.ErrShardNoData):
         enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 128, 0, 4)
+    # rows that overlap: a shard-major destination whose pitch
+    # is shorter than its objects' span (4 x 128-B pieces in a 400-B row)
+    with pytest.raises(ia.InvalidArgument):
+        enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 400, 128, 100, 4)
+    # object-major destination whose objects' rows run into the next object
+    with pytest.raises(ia.InvalidArgument):
+        enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 128, 11 * 128, 100, 4)
+    # ... and the same geometry on the source side
+    with pytest.raises(ia.InvalidArgument):
+        enc.copy_pieces(0x1000, 128, 11 * 128, 0x100000, 4096, 128, 100, 4)
+    # a pitch below shard_len with two rows moving
+    with pytest.raises(ia.InvalidArgument):
+        enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 64, 128 * 12, 100, 1, rows=[0, 1])
+    # the rows that move decide: only row 0 of an 11-row object stride is fine
+    if not ia.device_ok(0):
+        with pytest.raises(ia.NoDevice):
+            enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 128, 11 * 128, 100, 4, rows=[0, 10])
     if not ia.device_ok(0):
         with pytest.raises(ia.NoDevice):
             enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 128, 100, 4)

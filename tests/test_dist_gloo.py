@@ -99,3 +99,35 @@ def test_shard_objects_cover_all():
             spans = [bench.shard_objects(n, r, world) for r in range(world)]
             assert sum(c for _, c in spans) == n
             assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def _one_rank(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import bench
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        d = bench.DistCtx(1, 0, "cpu", force=True)
+        el = bench.timed_run(lambda i: time.sleep(0.01), steps=2, warmup=1, sync=lambda: None, dctx=d)
+        q.put((el, d.sum(7), d.gather(0.25), d.calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_forced_collectives_at_world_one():
+    """--collectives: DistCtx issues its collectives over a one-rank process
+    group (the RCCL path of BENCH config 4 on a one-GPU box), same results
+    as the short-circuited form."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_one_rank, args=(_free_port(), q))
+    p.start()
+    el, s, g, calls = q.get(timeout=120)
+    p.join(60)
+    assert p.exitcode == 0
+    assert el >= 0.02 and s == 7 and g == [0.25]
+    assert calls == 2 + 1 + 1 + 1  # timed_run's two barriers and MAX, the SUM, the gather
+    import bench
+    d0 = bench.DistCtx(1, 0, "cpu")
+    assert not d0.on and d0.max(1.5) == 1.5 and d0.gather(2.0) == [2.0] and d0.calls == 0

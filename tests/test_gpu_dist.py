@@ -144,3 +144,46 @@ def test_bench_two_ranks_shared_gpu(gpu, tmp_path):
     assert cpu is not None and cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
     assert "bit-exact vs GPU" in cpu["sample"] and cpu["sample"].endswith(": True"), cpu["sample"]
     assert out["roofline"]["traffic_source"].startswith(("committed profile", "none"))
+    assert out["roofline"]["frac_per_rank"] and len(out["roofline"]["frac_per_rank"]) == 2
+    # strong scaling beside the weak line: the 48-object
+    # batch split 24 + 24 over the two ranks, every object coded once
+    st = out["strong_scaling"]
+    assert st["batch_total"] == 48 and st["objects_coded"] == 48 and st["objects_per_rank"] == [24, 24]
+    assert st["value"] > 0 and st["ms_per_step"] > 0
+
+
+def test_bench_one_rank_rccl(gpu):
+    """BASELINE config 4's collectives on the one-GPU box: bench.py under
+    torch.distributed.run with ONE rank, the default nccl (RCCL) backend and
+    the collectives forced on at world size 1: init_process_group with
+    device_id, the device-tensor barrier, the float64 MAX-reduce, the int64
+    SUM and the one-hot gather all execute over RCCL."""
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    env.pop("BENCH_DIST_BACKEND", None)
+    env.pop("BENCH_SHARE_GPU", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--collectives", "--steps", "5", "--warmup", "3",
+           "--batch", "64", "--cpu-seconds", "2", "--no-pmc"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["config"]["batch_per_gpu"] == 64
+    assert "RCCL all_reduce barrier only" in out["config"]["parallelism"], out["config"]["parallelism"]
+    # weak and strong regions: 2 barriers + MAX each, a SUM each, the strong
+    # block's gather and the roofline gather
+    assert out["collectives_issued"] >= 8
+    assert out["decode_check"] == "bit-exact"
+    assert all(v["result"] == "bit-exact" for v in out["work_check"].values())
+    assert len(out["roofline"]["frac_per_rank"]) == 1 and out["roofline"]["frac_per_rank"][0] > 0
+    st = out["strong_scaling"]
+    assert st["objects_coded"] == 64 and st["objects_per_rank"] == [64]
+    cpu = out["cpu_baseline"]
+    assert cpu is not None and cpu["kind"] == "port" and cpu["value"] > 0
+    assert cpu["sample"].endswith(": True"), cpu["sample"]
+    dst = os.environ.get("BENCH_RCCL_JSON")
+    if dst:  # the committed evidence (profiles/r05_bench_rccl_1rank.json)
+        with open(dst, "w") as f:
+            f.write(lines[0] + "\n")

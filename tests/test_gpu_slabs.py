@@ -2,13 +2,13 @@
 
 Upstream's reedsolomon.Encoder codes shards of any length.  A pass addresses
 its staged image with 32-bit offsets, so the per-object host calls code an
-object whose staged image passes the slab size (1 GiB; RSGPU_SLAB_BYTES
+object whose staged image passes the slab size (1 GiB; rsgpu_set_slab_bytes / RSGPU_SLAB_BYTES
 overrides it) as consecutive column slabs of every row, and the batch
 pipelines hand such objects to that path.  Every operation is a byte-column
 map, so the result must equal the unslabbed oracle's bit for bit; check
 flags are OR-ed over the slabs.
 
-Small objects with RSGPU_SLAB_BYTES = 64 KiB exercise every operation with
+Small objects with the slab size set to 64 KiB (rsgpu_set_slab_bytes) exercise every operation with
 several slabs (incl. a ragged last one) against the oracle; one RS(10+2)
 object of 12 x 360 MiB (a 4.2 GB Split image, past what one pass addresses)
 runs at the default slab size, checked on column windows around every slab
@@ -27,9 +27,13 @@ SEED = 0x51AB
 
 
 @pytest.fixture
-def small_slabs(monkeypatch):
-    monkeypatch.setenv("RSGPU_SLAB_BYTES", str(64 << 10))
-    yield 64 << 10
+def small_slabs():
+    # the library reads the slab size once; tests set it through the C ABI
+    ia.set_slab_bytes(64 << 10)
+    try:
+        yield 64 << 10
+    finally:
+        ia.set_slab_bytes(0)
 
 
 def _full(k, p, size, idx):

@@ -528,12 +528,12 @@ def _large_pageable_case(rng, counts):
 
 def _slab_case(rng, counts):
     """a host op with a small slab size: the object is coded in column slabs"""
-    os.environ["RSGPU_SLAB_BYTES"] = str(int(rng.integers(4096, 1 << 16)))
+    ia.set_slab_bytes(int(rng.integers(4096, 1 << 16)))
     try:
         _host_case(rng, counts)
         counts["slabs"] += 1
     finally:
-        del os.environ["RSGPU_SLAB_BYTES"]
+        ia.set_slab_bytes(0)
 
 
 def test_gpu_soak_vs_oracle(gpu):

@@ -167,10 +167,11 @@ def test_worker_busy_beside_stream_path_growth_and_wide_masks(gpu):
 
 def test_worker_busy_beside_user_pinned_alloc_free(gpu):
     """rsgpu_host_free / rsgpu_host_register / _unregister from the user (the
-    Go shim's stage pool frees C-owned images) while the worker is busy: the
-    workers are parked around the device-synchronising call, so it returns
-    promptly; the busy callers are declined to the stream path meanwhile and
-    stay exact."""
+    Go shim's stage pool frees C-owned images) while the worker is busy:
+    a free is held back until no worker kernel is resident and
+    an unregister parks the workers around the device-synchronising call, so
+    each returns promptly; the busy callers are declined to the stream path
+    during a park and stay exact."""
     import ctypes
     enc = ia.New(K, P)
     enc.worker_start(nslots=8)
@@ -238,3 +239,59 @@ def test_worker_two_contexts_one_stops(gpu):
         dt = time.monotonic() - t0
     assert dt < 2.0, dt
     b.worker_stop()
+
+
+def test_retired_frees_stay_bounded(gpu):
+    """while a worker kernel is resident, the library's
+    own frees (staging buffers that grew, contexts destroyed) are held back
+    so they never wait for it — and what is held stays bounded: past
+    kKeptCap (256 MiB) the workers are parked and everything held is freed
+    (devmem.cpp relieve_retired).  Once no worker kernel is resident, the
+    next free lets go of everything held; frees are held only while a kernel
+    is resident, not merely while a worker is started."""
+    import ctypes
+    import gc
+    cap = 256 << 20
+    enc = ia.New(K, P)
+    enc.worker_start(nslots=8, idle_us=2000)
+    L = ia._lib.load()
+    peak = 0
+    d0 = ia.retired_stats()["deferred"]
+    with _Busy(enc) as busy:
+        assert not busy.errors, busy.errors[:2]
+        for i in range(10):
+            c = ia.New(K, P)  # its staging grows to ~2 x 29 MB, freed (held) at destroy
+            for size in (4 << 20, 24 << 20):
+                obj = rn.splitmix64_bytes(0xB0B, 10 * i + size, size)
+                sh = c.Split(obj)
+                c.Encode(sh)
+                e, want = oracle.encode(K, P, [bytes(s) for s in sh[:K]] + [bytes(len(sh[0]))] * P)
+                assert e == 0 and all(np.array_equal(sh[K + r], want[K + r]) for r in range(P))
+            del c
+            gc.collect()
+            st = ia.retired_stats()
+            peak = max(peak, st["bytes"])
+            assert st["bytes"] <= cap + (128 << 20), st  # the cap plus one context's buffers
+        held = ia.retired_stats()["deferred"] - d0
+    assert not busy.errors, busy.errors[:2]
+    assert held > 0  # the kernel was resident: frees were held back
+    assert peak >= 32 << 20  # ... including the destroyed contexts' staging images
+    # the busy callers stopped: the kernel leaves after idle_us (2 ms); the
+    # next free finds none resident and lets go of everything held
+    time.sleep(0.1)
+    p = ctypes.c_void_p()
+    assert L.rsgpu_host_alloc(1 << 16, ctypes.byref(p)) == 0
+    assert L.rsgpu_host_free(p) == 0
+    st = ia.retired_stats()
+    print(f"held back while resident: {held} frees, peak {peak >> 20} MiB; after idle: {st}")
+    assert st["count"] == 0 and st["bytes"] == 0, st
+    # started but idle: a free runs at once (nothing is held)
+    d1 = st["deferred"]
+    c = ia.New(K, P)
+    sh = c.Split(rn.splitmix64_bytes(0xB0C, 1, 1 << 20))
+    c.Encode(sh)
+    del c
+    gc.collect()
+    st = ia.retired_stats()
+    assert st["deferred"] == d1 and st["count"] == 0, st
+    enc.worker_stop()

@@ -62,8 +62,19 @@ PY
               LAT_WORKER=16 LAT_BYTES=$b run lat_worker_vram_$b 120 ./tools/lat_bench 200 1
               RSGPU_WORKER_TRANSPORT=host LAT_WORKER=16 LAT_BYTES=$b run lat_worker_host_$b 120 ./tools/lat_bench 200 1
             done ;;
-    lat_alloc) LAT_BYTES=1048576 run lat_stream_1m_default 120 ./tools/lat_bench 200 1
-            RSGPU_HOST_ALLOC=coherent LAT_BYTES=1048576 run lat_stream_1m_coherent 120 ./tools/lat_bench 200 1 ;;
+    lat_alloc) # host image allocation kinds, interleaved: Mapped|Coherent (default since r05) vs hipHostMallocDefault
+            for rep in 1 2; do
+              LAT_BYTES=1048576 run lat_1m_coherent_$rep 120 ./tools/lat_bench 300 1
+              RSGPU_HOST_ALLOC=default LAT_BYTES=1048576 run lat_1m_default_$rep 120 ./tools/lat_bench 300 1
+              LAT_WORKER=16 LAT_BYTES=1024 run lat_1k_coherent_$rep 120 ./tools/lat_bench 300 1
+              RSGPU_HOST_ALLOC=default LAT_WORKER=16 LAT_BYTES=1024 run lat_1k_default_$rep 120 ./tools/lat_bench 300 1
+            done ;;
+    trace_alloc) run trace_coherent 900 python bench.py --workload trace --steps 3 --warmup 1
+            RSGPU_HOST_ALLOC=default run trace_default 900 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu ;;
+    tests)  # a chosen set of GPU test files (TESTS), one pytest process
+            run pytest_sel 900 python -u -m pytest ${TESTS} -m gpu -x -v -s --timeout 150 --timeout-method thread ;;
+    rccl1)  # BASELINE config 4's collectives over RCCL with one rank (the -m gpu test writes the line)
+            BENCH_RCCL_JSON=gpurun_out/r05_bench_rccl_1rank.json run pytest_rccl1 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -x -v -s --timeout 240 --timeout-method thread ;;
     avail)  run avail 120 rocprofv3 --list-avail ;;
     pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
