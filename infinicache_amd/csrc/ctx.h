@@ -30,9 +30,15 @@ struct Slot {
     uint8_t *hdev = nullptr;  // device address of the pinned staging image h
     size_t cap = 0;
     hipStream_t stream = nullptr;
+    // a second stream (and its event) for the copy-engine share of a split
+    // per-object call (rsgpu.cpp run_host_once, RSGPU_DMA_SPLIT)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev2 = nullptr;
     uint32_t *d_bad = nullptr, *h_bad = nullptr;
     uint32_t *m_bad = nullptr;  // device address of h_bad (mapped pinned memory)
     ~Slot() {
+        if (ev2) (void)hipEventDestroy(ev2);
+        if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
         retire(h, true, cap);
         retire(d, false, cap);

@@ -135,6 +135,19 @@ int check_shards(const size_t *lens, int n, bool nilok, size_t *size) {
 
 namespace {
 
+// The copy-engine share of a split per-object call, percent of the columns
+// (run_host_once; RSGPU_DMA_SPLIT, read once; 0 = off), for objects whose
+// shards are at least kDmaSplitMin bytes
+constexpr size_t kDmaSplitMin = (size_t)64 << 10;
+int dma_split_pct() {
+    static const int v = [] {
+        const char *e = std::getenv("RSGPU_DMA_SPLIT");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 && x < 100 ? x : 0;
+    }();
+    return v;
+}
+
 // Runs `plan` over one object staged from host buffers.  in_src[c] is the
 // host source of staging row plan.in_rows[c]; out_dst[r] receives written
 // row r.  Returns the mismatch flag in *bad when the plan has check rows.
@@ -183,6 +196,7 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         return j;
     };
     hipError_t he = hipSuccess;
+    bool staged_in = false;  // the inputs were copied into the slot's pinned image s->h
     const uint8_t *span0 = in_src[0] - (size_t)(plan.in_rows[0] - rlo) * size;
     bool split = pin_in;
     for (int c = 0; c < plan.K && split; ++c)
@@ -220,6 +234,7 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         std::vector<CopyJob> cp((size_t)plan.K);
         for (int c = 0; c < plan.K; ++c) cp[c] = {s->h + (size_t)plan.in_rows[c] * size, in_src[c], size};
         copy_rows(cp.data(), cp.size());
+        staged_in = true;
         if (plan.K <= kRedirectMaxK && s->hdev) {
             // the pass reads the pinned staging image in place (zero-copy);
             // the slot holds nrows_staged*size + 16 bytes at least
@@ -261,7 +276,52 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         L.out_base = s->hdev;
         L.out_dual = then != nullptr;
     }
+    // Copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent>): a
+    // pass reading host memory moves ~36 GB/s, a DMA ~55 GB/s
+    // (profiles/r04_redirect_bs_sweep.txt, r01_pcie_bench.txt), so the input
+    // rows' last columns [cb, size) go H2D on a second stream and a second
+    // pass codes them from HBM while the first pass codes columns [0, cb)
+    // over PCIe.  Every operation is a byte-column map.  The second share is
+    // whole 16-B vectors, so its last vector ends at the row's end; the first
+    // share's last vector may reach into the second's first vector, where
+    // both passes store the same bytes (the coding of the same input
+    // columns).  Both passes set the same mapped check flag.
+    bool two = false;
+    if (he == hipSuccess && L.in_base && size >= kDmaSplitMin && dma_split_pct() > 0) {
+        const size_t blen = (size * (size_t)dma_split_pct() / 100) & ~(size_t)15;
+        if (blen >= 4096 && blen + 16 <= size) {
+            const size_t cb = size - blen;
+            if (!s->stream2 && (he = hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking)) != hipSuccess)
+                s->stream2 = nullptr;
+            if (he == hipSuccess && !s->ev2 && (he = hipEventCreateWithFlags(&s->ev2, hipEventDisableTiming)) != hipSuccess)
+                s->ev2 = nullptr;
+            for (int c = 0; c < plan.K && he == hipSuccess; ++c) {
+                const size_t ro = (size_t)plan.in_rows[c] * size;
+                const uint8_t *src = staged_in ? s->h + ro : in_src[c];
+                he = hipMemcpyAsync(s->d + ro + cb, src + cb, blen, hipMemcpyHostToDevice, s->stream2);
+            }
+            if (he == hipSuccess) {
+                Layout B{s->d + cb, 0, size, blen, 1};
+                B.slack = true;
+                if (L.out_base) {
+                    B.out_base = L.out_base + cb;
+                    B.out_dual = L.out_dual;
+                }
+                he = launch_plan(plan, B, s->m_bad, s->stream2);
+            }
+            if (he == hipSuccess) {
+                L.shard_len = cb;
+                two = true;
+            }
+        }
+    }
     if (he == hipSuccess) he = launch_plan(plan, L, s->m_bad, s->stream);
+    // what follows on the slot's stream (D2H of written rows, the `then`
+    // pass over the image) waits for the second share
+    if (two && he == hipSuccess && (!L.out_base || then)) {
+        he = hipEventRecord(s->ev2, s->stream2);
+        if (he == hipSuccess) he = hipStreamWaitEvent(s->stream, s->ev2, 0);
+    }
     auto dst = [&](size_t r) {
         return pin_out ? (const uint8_t *)out_dst[r] : (const uint8_t *)s->h + (size_t)orows[r] * size;
     };
@@ -281,9 +341,11 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         img.slack = true;
         he = launch_plan(*then, img, s->m_bad, s->stream);
     }
+    if (he == hipSuccess && two) he = hipStreamSynchronize(s->stream2);
     if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
     if (he != hipSuccess) {
         (void)hipStreamSynchronize(s->stream);  // nothing in flight may touch a pooled slot
+        if (s->stream2) (void)hipStreamSynchronize(s->stream2);
         ctx->put_slot(std::move(s));
         return hip_fail(he, "run_host");
     }

@@ -71,6 +71,13 @@ PY
             done ;;
     trace_alloc) run trace_coherent 900 python bench.py --workload trace --steps 3 --warmup 1
             RSGPU_HOST_ALLOC=default run trace_default 900 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu ;;
+    dma_split) # the copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent of columns>), 1 MiB per object
+            RSGPU_DMA_SPLIT=40 run pytest_dma_split 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random.py tests/test_c_abi.py -m gpu -x -q --timeout 150 --timeout-method thread
+            for rep in 1 2; do
+              for pct in ${DMA_PCTS:-0 20 30 40 50}; do
+                RSGPU_DMA_SPLIT=$pct LAT_BYTES=${DMA_BYTES:-1048576} run lat_dma_${pct}_$rep 120 ./tools/lat_bench 300
+              done
+            done ;;
     tests)  # a chosen set of GPU test files (TESTS), one pytest process
             run pytest_sel 900 python -u -m pytest ${TESTS} -m gpu -x -v -s --timeout 150 --timeout-method thread ;;
     rccl1)  # BASELINE config 4's collectives over RCCL with one rank (the -m gpu test writes the line)
