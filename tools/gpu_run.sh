@@ -78,6 +78,13 @@ PY
                 RSGPU_DMA_SPLIT=$pct LAT_BYTES=${DMA_BYTES:-1048576} run lat_dma_${pct}_$rep 120 ./tools/lat_bench 300
               done
             done ;;
+    wslice) # large pinned objects as column slices over many mailboxes (worker) vs the stream path
+            for b in ${WS_BYTES:-262144 1048576 4194304}; do
+              LAT_BYTES=$b run ws_stream_$b 120 ./tools/lat_bench 300
+              for ns in ${WS_SLOTS:-16 64}; do
+                RSGPU_WORKER_SPLIT_MAX=4194304 LAT_WORKER=$ns LAT_MAX_SHARD=4096 LAT_BYTES=$b run ws_w${ns}_$b 120 ./tools/lat_bench 300
+              done
+            done ;;
     tests)  # a chosen set of GPU test files (TESTS), one pytest process
             run pytest_sel 900 python -u -m pytest ${TESTS} -m gpu -x -v -s --timeout 150 --timeout-method thread ;;
     rccl1)  # BASELINE config 4's collectives over RCCL with one rank (the -m gpu test writes the line)
