@@ -588,14 +588,17 @@ def run_latency(args):
     """The per-object path the Go shim takes (one EcSet / EcGet at a time,
     host buffers in and out): Client.encode = Encode + Verify
     (ecRedis.go:382-402) and Client.decode = Reconstruct + Verify of 2 lost
-    data shards, fused (ecRedis.go:404-427), on 1 MiB RS(10+2) objects.
+    data shards, fused (ecRedis.go:404-427), on RS(10+2) objects of
+    --obj-bytes (1 MiB), from Python (the C ABI's own figures: tools/lat_bench).
     Reports per-op latency percentiles beside the CPU port's per-object
     codeSomeShardsP latency.  A DESIGN.md measurement, not the headline."""
     import infinicache_amd as ia
     import oracle
     from oracle import rs_numpy as rn
-    k, p, nb = 10, 2, 1 << 20
+    k, p, nb = 10, 2, args.obj_bytes
     enc = ia.New(k, p)
+    if args.worker:
+        enc.worker_start(nslots=args.worker)
     rng = np.random.default_rng(7)
     nobj = 64
     objs = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(nobj)]
@@ -648,8 +651,13 @@ def run_latency(args):
         if it >= args.warmup:
             ce.append(t1 - t0)
             cd.append(t2 - t1)
+    from infinicache_amd import ec
     out = {
-        "metric": "RS(10+2) per-object host-API latency (Client.encode / Client.decode), 1 MiB objects",
+        "metric": f"RS(10+2) per-object host-API latency (Client.encode / Client.decode), {nb} B objects, "
+                  f"from Python",
+        "python_marshalling": "C (csrc/pyshards.c)" if ec._pyshards is not None else "ctypes",
+        "worker_mailboxes": args.worker,
+        "worker_stats": enc.worker_stats() if args.worker else None,
         "gpu": res,
         "cpu_port_16_threads": {
             "encode_verify_us_p50": round(float(np.percentile(ce, 50)) * 1e6, 1),
@@ -668,6 +676,8 @@ def main():
                          "clock ramps over the first ~0.1 s of load; 3 for trace/latency)")
     ap.add_argument("--workload", default="encdec", choices=sorted(WORKLOADS) + ["trace", "latency"])
     ap.add_argument("--trace-objects", type=int, default=512)
+    ap.add_argument("--obj-bytes", type=int, default=1 << 20, help="latency: object size")
+    ap.add_argument("--worker", type=int, default=0, help="latency: resident worker mailboxes (0: stream path)")
     ap.add_argument("--devices", type=int, default=1,
                     help="trace: GPUs driven by ONE process through a multi-device context")
     ap.add_argument("--batch", type=int, default=0, help="objects per GPU (default: workload's)")

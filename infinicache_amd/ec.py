@@ -22,6 +22,7 @@ pointer (int) or any object with ``data_ptr()`` (a torch tensor) laid out
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -161,6 +162,34 @@ class _ShardTable:
         self.lens = (ctypes.c_size_t * n)(*[len(a) if a is not None else 0 for a in arrs])
 
 
+# The per-object calls marshal their shard table in C when the in-tree
+# extension is built (csrc/pyshards.c: buffer protocol + a direct call of the
+# rsgpu entry point, GIL released); without it, or for a buffer it cannot
+# take as one contiguous byte range, _ShardTable does it through ctypes.
+try:
+    from . import _pyshards
+except ImportError:  # pragma: no cover - the Makefile builds it beside librsgpu.so
+    _pyshards = None
+if os.environ.get("INFINICACHE_PY_MARSHAL") == "ctypes":  # A/B measurement
+    _pyshards = None
+
+_FN_ADDR = {}
+
+
+def _fn_addr(L, name: str) -> int:
+    a = _FN_ADDR.get(name)
+    if a is None:
+        a = _FN_ADDR[name] = ctypes.cast(getattr(L, name), ctypes.c_void_p).value
+    return a
+
+
+def _fast_call(L, name: str, ctx, shards, wlo: int, whi: int, missing, kind: int, arg: int = 0):
+    """_pyshards.call, or None when the ctypes path must take the call."""
+    if _pyshards is None or not ctx:
+        return None
+    return _pyshards.call(_fn_addr(L, name), ctx.value or 0, shards, wlo, whi, missing, kind, arg)
+
+
 def _dptr(x) -> int:
     if x is None:
         return 0
@@ -254,10 +283,18 @@ class RSEncoder:
 
     # -- the 7 reedsolomon.Encoder methods -------------------------------
     def Encode(self, shards: Sequence) -> None:
+        r = _fast_call(self._L, "rsgpu_encode", self._ctx, shards, self.DataShards, len(shards), None, 2)
+        if r is not None:
+            _check(r)
+            return
         t = _ShardTable(shards, writable_idx=range(self.DataShards, len(shards)))
         _check(self._L.rsgpu_encode(self._ctx, t.ptrs, t.lens, len(shards)))
 
     def Verify(self, shards: Sequence) -> bool:
+        r = _fast_call(self._L, "rsgpu_verify", self._ctx, shards, 0, 0, None, 1)
+        if r is not None:
+            _check(r[0])
+            return bool(r[1])
         t = _ShardTable(shards)
         ok = ctypes.c_int(0)
         _check(self._L.rsgpu_verify(self._ctx, t.ptrs, t.lens, len(shards), ctypes.byref(ok)))
@@ -267,6 +304,10 @@ class RSEncoder:
         """Client.encode's Encode then Verify (ecRedis.go:390-395) in one
         device round trip: parity written into shards[k:], then every parity
         shard re-checked on the device image; returns Verify's boolean."""
+        r = _fast_call(self._L, "rsgpu_encode_verify", self._ctx, shards, self.DataShards, len(shards), None, 1)
+        if r is not None:
+            _check(r[0])
+            return bool(r[1])
         t = _ShardTable(shards, writable_idx=range(self.DataShards, len(shards)))
         ok = ctypes.c_int(0)
         _check(self._L.rsgpu_encode_verify(self._ctx, t.ptrs, t.lens, len(shards), ctypes.byref(ok)))
@@ -291,18 +332,30 @@ class RSEncoder:
         if not isinstance(shards, list):
             raise InvalidArgument("shards must be a list (filled in place)")
         bufs, missing = self._prepare_missing(shards, data_only)
-        t = _ShardTable(bufs, writable_idx=missing)
-        for i in missing:
-            t.lens[i] = 0  # "missing": the buffer is the output
         n = len(shards)
-        ok = ctypes.c_int(1)
+        # "missing": passed with length 0, the buffer is the output
         if fused_verify:
-            _check(self._L.rsgpu_decode(self._ctx, t.ptrs, t.lens, n, ctypes.byref(ok)))
+            r = _fast_call(self._L, "rsgpu_decode", self._ctx, bufs, 0, 0, missing, 1)
         else:
-            _check(self._L.rsgpu_reconstruct(self._ctx, t.ptrs, t.lens, n, int(data_only)))
+            r = _fast_call(self._L, "rsgpu_reconstruct", self._ctx, bufs, 0, 0, missing, 0, int(data_only))
+        if r is not None:
+            ok_v = 1
+            if fused_verify:
+                r, ok_v = r
+            _check(r)
+        else:
+            t = _ShardTable(bufs, writable_idx=missing)
+            for i in missing:
+                t.lens[i] = 0
+            ok = ctypes.c_int(1)
+            if fused_verify:
+                _check(self._L.rsgpu_decode(self._ctx, t.ptrs, t.lens, n, ctypes.byref(ok)))
+            else:
+                _check(self._L.rsgpu_reconstruct(self._ctx, t.ptrs, t.lens, n, int(data_only)))
+            ok_v = ok.value
         for i in missing:
             shards[i] = bufs[i]
-        return bool(ok.value)
+        return bool(ok_v)
 
     def Reconstruct(self, shards: list) -> None:
         self._reconstruct(shards, data_only=False, fused_verify=False)

@@ -85,3 +85,56 @@ def test_new_encoder_factory(capsys):
     assert isinstance(ia.NewEncoder(10, 2, 32), ia.RSEncoder)
     assert ia.NewEncoder(0, 2, 32) is None  # error printed and swallowed
     assert "newEncoder err" in capsys.readouterr().out
+
+
+def _outcome(fn):
+    try:
+        return ("ok", fn())
+    except Exception as e:  # noqa: BLE001 - the class is the result
+        return ("raise", type(e).__name__)
+
+
+def test_c_marshalling_matches_ctypes_path(monkeypatch):
+    """The per-object calls marshal their shard table in C
+    (csrc/pyshards.c) when the extension is built; every argument case ends
+    exactly as through the ctypes table (the same upstream error, the same
+    NoDevice on a GPU-less host, the same refusal of read-only or
+    non-contiguous outputs, the same copy of a non-contiguous input)."""
+    from infinicache_amd import ec
+    assert ec._pyshards is not None, "csrc/pyshards.c not built (make -C infinicache_amd/csrc)"
+    k, p, S = 10, 2, 103
+    n = k + p
+
+    def split():
+        b = np.zeros(n * S, np.uint8)
+        b[:k * S] = np.arange(k * S) % 251
+        return [b[i * S:(i + 1) * S] for i in range(n)]
+
+    strided = np.zeros(2 * S, np.uint8)[::2]
+    cases = {
+        "encode ok": lambda e: e.Encode(split()),
+        "encode 11 shards": lambda e: e.Encode(split()[:11]),
+        "encode size mismatch": lambda e: e.Encode(split()[:-1] + [np.zeros(S + 1, np.uint8)]),
+        "encode all empty": lambda e: e.Encode([np.zeros(0, np.uint8)] * n),
+        "encode read-only parity": lambda e: e.Encode(split()[:k] + [bytes(S)] * p),
+        "encode strided parity": lambda e: e.Encode(split()[:k] + [strided, np.zeros(S, np.uint8)]),
+        "encode strided input": lambda e: e.Encode([strided] + split()[1:]),
+        "encode bytes inputs": lambda e: e.Encode([bytes(x) for x in split()[:k]] + [bytearray(S)] * p),
+        "verify ok": lambda e: e.Verify(split()),
+        "verify nil shard": lambda e: e.Verify([None] + split()[1:]),
+        "encode+verify ok": lambda e: e.EncodeVerify(split()),
+        "decode ok": lambda e: e.DecodeVerify([None if i in (0, 5) else s for i, s in enumerate(split())]),
+        "decode too few": lambda e: e.DecodeVerify([None if i < 3 else s for i, s in enumerate(split())]),
+        "reconstruct ok": lambda e: e.Reconstruct([None if i in (1, 11) else s for i, s in enumerate(split())]),
+        "reconstruct data": lambda e: e.ReconstructData([None if i in (1, 11) else s for i, s in enumerate(split())]),
+        "reconstruct size mismatch": lambda e: e.Reconstruct([None] + split()[1:-1] + [np.zeros(S + 2, np.uint8)]),
+    }
+    enc = ia.New(k, p)
+    fast = {name: _outcome(lambda: f(enc)) for name, f in cases.items()}
+    monkeypatch.setattr(ec, "_pyshards", None)
+    slow = {name: _outcome(lambda: f(enc)) for name, f in cases.items()}
+    assert fast == slow
+    if not ia.device_ok(0):
+        assert fast["encode ok"] == ("raise", "NoDevice")
+        assert fast["encode 11 shards"] == ("raise", "ErrTooFewShards")
+        assert fast["encode read-only parity"] == ("raise", "InvalidArgument")

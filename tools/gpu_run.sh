@@ -85,6 +85,13 @@ PY
                 RSGPU_WORKER_SPLIT_MAX=4194304 LAT_WORKER=$ns LAT_MAX_SHARD=4096 LAT_BYTES=$b run ws_w${ns}_$b 120 ./tools/lat_bench 300
               done
             done ;;
+    pylat)  # per-object latency from Python: C marshalling (default) vs ctypes, 1 KiB via the worker and 1 MiB
+            for rep in 1 2; do
+              run pylat_1k_c_$rep 300 python bench.py --workload latency --steps 300 --warmup 20 --obj-bytes 1024 --worker 16
+              INFINICACHE_PY_MARSHAL=ctypes run pylat_1k_ctypes_$rep 300 python bench.py --workload latency --steps 300 --warmup 20 --obj-bytes 1024 --worker 16
+              run pylat_1m_c_$rep 300 python bench.py --workload latency --steps 200 --warmup 10
+              INFINICACHE_PY_MARSHAL=ctypes run pylat_1m_ctypes_$rep 300 python bench.py --workload latency --steps 200 --warmup 10
+            done ;;
     tests)  # a chosen set of GPU test files (TESTS), one pytest process
             run pytest_sel 900 python -u -m pytest ${TESTS} -m gpu -x -v -s --timeout 150 --timeout-method thread ;;
     rccl1)  # BASELINE config 4's collectives over RCCL with one rank (the -m gpu test writes the line)
