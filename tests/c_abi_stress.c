@@ -187,6 +187,16 @@ int main(int argc, char **argv) {
     pthread_t th[64];
     const int nt = threads < 1 ? 1 : threads > 64 ? 64 : threads;
     for (long i = 0; i < nt; i++) pthread_create(&th[i], NULL, thread_main, (void *)i);
+    /* the frees the library holds back while the worker kernel is resident
+     * (devmem.cpp) stay bounded: 256 MiB plus what one call can retire */
+    size_t peak = 0, cnt = 0, bytes = 0;
+    uint64_t deferred = 0;
+    while (now_s() < deadline) {
+        rsgpu_retired_stats(&cnt, &bytes, &deferred);
+        if (bytes > peak) peak = bytes;
+        const struct timespec ts = {0, 5000000};
+        nanosleep(&ts, NULL);
+    }
     long bad = 0;
     for (int i = 0; i < nt; i++) {
         void *r;
@@ -196,6 +206,13 @@ int main(int argc, char **argv) {
     uint64_t served = 0, declined = 0, launches = 0;
     rsgpu_worker_stats(ctx, &served, &declined, &launches);
     rsgpu_destroy(ctx);
+    rsgpu_retired_stats(&cnt, &bytes, &deferred);
+    printf("retired: peak %.1f MiB held, %llu frees held back in all, %zu held after destroy\n",
+           peak / 1048576.0, (unsigned long long)deferred, cnt);
+    if (peak > ((size_t)320 << 20) || cnt != 0) {
+        fprintf(stderr, "held-back frees unbounded or left over after the worker stopped\n");
+        bad = 1;
+    }
     long total = 0;
     for (int i = 0; i < ROUTES; i++) total += counts[i];
     printf("stress: RS(%d+%d)%s, %d threads, %.0f s, %ld objects (routes:", K, P, KIND ? " Cauchy" : "", nt, seconds,
