@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <limits>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -45,6 +46,42 @@ int pipe_slots() {
         return v >= 1 && v <= 16 ? v : kSlots;
     }();
     return n;
+}
+
+// Adjacent small objects share one H2D (RSGPU_PIPE_GROUP=<bytes per group>,
+// read once; 0 = off).  A copy command carries a fixed ≈14 us
+// (tools/pcie_bench: back-to-back 1 MiB H2D at 32 GB/s, 512 MiB at 57), so a
+// batch of objects that lie back to back in host memory (Split images of one
+// arena) moves its small ones — images up to kGroupObjMax — as one copy of
+// their whole images, each then coded in place in the slot; written rows go
+// back per object.
+constexpr size_t kGroupObjMax = (size_t)4 << 20;
+size_t group_bytes() {
+    static const size_t v = [] {
+        const char *e = std::getenv("RSGPU_PIPE_GROUP");
+        const long long b = e ? std::atoll(e) : 0;
+        return b > 0 ? (size_t)b : (size_t)0;
+    }();
+    return v;
+}
+
+// [i, end) of `piped`: objects adjacent in host memory (image o+1 starts
+// where image o ends), each image at most kGroupObjMax, the span at most
+// group_bytes(); a single object when grouping is off.  img(o) / base(o):
+// an object's image bytes and first byte.
+template <class Img, class Base>
+size_t group_end(const std::vector<int> &piped, size_t i, Img img, Base base, size_t *span) {
+    size_t j = i + 1, sp = img(piped[i]);
+    const size_t G = group_bytes();
+    if (G && sp <= kGroupObjMax)
+        while (j < piped.size()) {
+            const int a = piped[j - 1], b = piped[j];
+            if (img(b) > kGroupObjMax || sp + img(b) > G || base(b) != base(a) + img(a)) break;
+            sp += img(b);
+            ++j;
+        }
+    *span = sp;
+    return j;
 }
 
 int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
@@ -263,19 +300,31 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
     if (piped.empty()) return RSGPU_OK;
     auto plan = ctx->plan_encode();
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
+    if (group_bytes()) maxbytes = std::max(maxbytes, group_bytes() + 16);
     if ((e = ensure_slots(ctx, maxbytes))) return e;
     hipError_t he = hipSuccess;
-    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++q) {
-        const int o = piped[q];
-        PipeSlot &s = *ctx->pipe.slots[q % pipe_slots()];
-        const size_t S = shard_lens[o];
-        he = hipMemcpyAsync(s.d, objs[o], (size_t)k * S, hipMemcpyHostToDevice, s.stream);
-        Layout L{s.d, 0, S, S, 1};
-        L.slack = true;  // slot capacity >= n*S + 16
-        if (he == hipSuccess) he = launch_plan(*plan, L, nullptr, s.stream);
-        if (he == hipSuccess)
-            he = hipMemcpyAsync(objs[o] + (size_t)k * S, s.d + (size_t)k * S, (size_t)p * S,
-                                hipMemcpyDeviceToHost, s.stream);
+    auto img = [&](int o) { return (size_t)n * shard_lens[o]; };
+    auto base = [&](int o) { return (const uint8_t *)objs[o]; };
+    size_t sq = 0;
+    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++sq) {
+        size_t span = 0;
+        const size_t qe = group_end(piped, q, img, base, &span);
+        PipeSlot &s = *ctx->pipe.slots[sq % pipe_slots()];
+        // one object: its k data rows; a group: the whole images
+        he = hipMemcpyAsync(s.d, objs[piped[q]], qe - q > 1 ? span : (size_t)k * shard_lens[piped[q]],
+                            hipMemcpyHostToDevice, s.stream);
+        for (size_t off = 0; q < qe && he == hipSuccess; ++q) {
+            const int o = piped[q];
+            const size_t S = shard_lens[o];
+            Layout L{s.d + off, 0, S, S, 1};
+            L.slack = true;  // slot capacity >= n*S + 16 past the image
+            he = launch_plan(*plan, L, nullptr, s.stream);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(objs[o] + (size_t)k * S, s.d + off + (size_t)k * S, (size_t)p * S,
+                                    hipMemcpyDeviceToHost, s.stream);
+            off += (size_t)n * S;
+        }
+        q = qe;
     }
     e = drain(ctx);
     if (he != hipSuccess) return hip_fail(he, "rsgpu_encode_batch");
@@ -345,12 +394,51 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
     }
     if (piped.empty()) return RSGPU_OK;
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
+    if (group_bytes()) maxbytes = std::max(maxbytes, group_bytes() + 16);
     if ((e = ensure_slots(ctx, maxbytes))) return e;
     if ((e = ensure_flags(ctx, nobj))) return e;
     hipError_t he = hipSuccess;
-    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++q) {
-        const int o = piped[q];
-        PipeSlot &s = *ctx->pipe.slots[q % pipe_slots()];
+    // grouping (RSGPU_PIPE_GROUP): objects whose shards form one Split image
+    // each, back to back in host memory, and whose plans have no check rows
+    // (a Get of exactly k bodies); the group's H2D carries every row, the
+    // absent ones included (the pass overwrites them)
+    auto split_image = [&](int o) {
+        uint8_t *const *row = shards + (size_t)o * n;
+        for (int i = 1; i < n; ++i)
+            if (row[i] != row[0] + (size_t)i * shard_lens[o]) return false;
+        return plans[o]->nw == plans[o]->R;
+    };
+    auto img = [&](int o) {
+        return group_bytes() && split_image(o) ? (size_t)n * shard_lens[o] : std::numeric_limits<size_t>::max();
+    };
+    auto base = [&](int o) { return (const uint8_t *)shards[(size_t)o * n]; };
+    size_t sq = 0;
+    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++sq) {
+        size_t span = 0;
+        const size_t qe = group_end(piped, q, img, base, &span);
+        PipeSlot &s = *ctx->pipe.slots[sq % pipe_slots()];
+        if (qe - q > 1) {
+            he = hipMemcpyAsync(s.d, base(piped[q]), span, hipMemcpyHostToDevice, s.stream);
+            for (size_t off = 0; q < qe && he == hipSuccess; ++q) {
+                const int o = piped[q];
+                Plan &plan = *plans[o];
+                uint8_t *const *row = shards + (size_t)o * n;
+                const size_t S = shard_lens[o];
+                he = launch_plan(plan, slack_layout(s.d + off, S, S), nullptr, s.stream);
+                for (int r = 0; r < plan.nw && he == hipSuccess;) {  // rebuilt rows, runs merged
+                    const int r0 = plan.out_rows[r];
+                    int m = 1;
+                    while (r + m < plan.nw && plan.out_rows[r + m] == r0 + m) ++m;
+                    he = hipMemcpyAsync(row[r0], s.d + off + (size_t)r0 * S, (size_t)m * S, hipMemcpyDeviceToHost,
+                                        s.stream);
+                    r += m;
+                }
+                ctx->pipe.h_bad[o] = 0;  // (no check rows)
+                off += (size_t)n * S;
+            }
+            continue;
+        }
+        const int o = piped[q++];
         Plan &plan = *plans[o];
         uint8_t *const *row = shards + (size_t)o * n;
         const size_t S = shard_lens[o], P = S;  // packed rows

@@ -12,6 +12,8 @@ host-memory edge cases, through the C ABI against the oracle (bit-exact).
   :161-173 gathered Get buffers), pinned and pageable.
 * Pinned user memory (rsgpu_host_register, no slack past the buffer) with a
   shard size that is not a multiple of 16."""
+import os
+
 import numpy as np
 import pytest
 
@@ -324,3 +326,85 @@ def test_pass_image_cache_keyed_by_shard_len(gpu):
         torch.cuda.synchronize()
         assert not bad.any()
         assert torch.equal(b[:, :, :S], golden[:, :, :S]), S
+
+
+_GROUP_CHILD = r'''
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import infinicache_amd as ia
+import oracle
+from oracle import rs_numpy as rn
+k, p = 10, 2
+n = k + p
+enc = ia.New(k, p)
+m = enc.matrix()
+rng = np.random.default_rng(7)
+# Split images back to back in one pinned arena: small ones (grouped), two
+# past kGroupObjMax (4 MiB images), and one gap that breaks the adjacency
+sizes = [4096, 4099, 70000, 1 << 20, 5 << 20, 333, 65536, 100, 4 << 20, 12345, 777777, 3000]
+Ss = [(nb + k - 1) // k for nb in sizes]
+offs = [0]
+for i, S in enumerate(Ss):
+    offs.append(offs[-1] + n * S + (4096 if i == 6 else 0))
+arena = ia.host_alloc(offs[-1])
+objs, datas = [], []
+for i, (nb, S) in enumerate(zip(sizes, Ss)):
+    img = arena[offs[i]:offs[i] + n * S]
+    img[:] = 0
+    img[:nb] = rn.splitmix64_bytes(0x5EED, 4000 + i, nb)
+    objs.append([img[j * S:(j + 1) * S] for j in range(n)])
+enc.encode_batch(objs)
+for sh in objs:
+    want = oracle.code_fast(m[k:], [sh[j] for j in range(k)], nthreads=8)
+    for r in range(p):
+        assert np.array_equal(sh[k + r], want[r]), "encode"
+golden = [[s.copy() for s in sh] for sh in objs]
+# Gets: exactly k bodies (grouped), 11 bodies (a check row: coded alone),
+# one of them with a corrupted extra shard (flag), and all 12 (Verify)
+present, expect_ok = [], []
+for i, sh in enumerate(objs):
+    pr = [True] * n
+    if i % 4 == 3:
+        lost = [int(x) for x in rng.choice(n, 1, replace=False)]
+    elif i == 10:
+        lost = []
+    else:
+        lost = [int(x) for x in rng.choice(n, 2, replace=False)]
+    for j in lost:
+        pr[j] = False
+        sh[j][:] = 0xA5
+    ok = True
+    if i == 7:  # corrupt a present parity shard beyond the survivors
+        extra = [j for j in range(n) if pr[j]][k:]
+        if extra:
+            sh[extra[0]][0] ^= 1
+            ok = False
+    present.append(pr)
+    expect_ok.append(ok)
+got = enc.decode_batch(objs, present=present)
+assert got == expect_ok, (got, expect_ok)
+for i, (sh, gd) in enumerate(zip(objs, golden)):
+    for j in range(n):
+        if not present[i][j]:
+            assert np.array_equal(sh[j], gd[j]), ("decode", i, j)
+print("group ok", len(objs))
+'''
+
+
+@pytest.mark.parametrize("group", ["0", str(8 << 20), str(64 << 10)])
+def test_batches_group_adjacent_small_objects(gpu, group):
+    """RSGPU_PIPE_GROUP (read once, so a child process per setting): batches
+    of Split images back to back in one pinned arena move their small
+    objects as one H2D per group; every result equals the oracle's, Gets
+    with check rows (extra bodies, a corrupted one flagged) are coded alone,
+    a gap or an image past 4 MiB ends a group.  Off ("0") is the same batch
+    through the per-object copies."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RSGPU_PIPE_GROUP=group)
+    r = subprocess.run([sys.executable, "-c", _GROUP_CHILD, root], capture_output=True, text=True, timeout=240,
+                       env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:] + r.stdout
+    assert "group ok 12" in r.stdout

@@ -92,6 +92,12 @@ PY
               run pylat_1m_c_$rep 300 python bench.py --workload latency --steps 200 --warmup 10
               INFINICACHE_PY_MARSHAL=ctypes run pylat_1m_ctypes_$rep 300 python bench.py --workload latency --steps 200 --warmup 10
             done ;;
+    trace_group) # config 5 with adjacent small objects sharing one H2D (RSGPU_PIPE_GROUP bytes), interleaved
+            for rep in 1 2; do
+              for g in ${GROUPS_B:-0 16777216 67108864}; do
+                RSGPU_PIPE_GROUP=$g run trace_group_${g}_$rep 600 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu
+              done
+            done ;;
     tests)  # a chosen set of GPU test files (TESTS), one pytest process
             run pytest_sel 900 python -u -m pytest ${TESTS} -m gpu -x -v -s --timeout 150 --timeout-method thread ;;
     rccl1)  # BASELINE config 4's collectives over RCCL with one rank (the -m gpu test writes the line)
