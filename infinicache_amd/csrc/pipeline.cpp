@@ -48,18 +48,21 @@ int pipe_slots() {
     return n;
 }
 
-// Adjacent small objects share one H2D (RSGPU_PIPE_GROUP=<bytes per group>,
-// read once; 0 = off).  A copy command carries a fixed ≈14 us
-// (tools/pcie_bench: back-to-back 1 MiB H2D at 32 GB/s, 512 MiB at 57), so a
-// batch of objects that lie back to back in host memory (Split images of one
-// arena) moves its small ones — images up to kGroupObjMax — as one copy of
-// their whole images, each then coded in place in the slot; written rows go
-// back per object.
+// Adjacent small objects share one H2D (16 MiB groups; RSGPU_PIPE_GROUP=
+// <bytes> overrides, 0 = off; read once).  A copy command carries a fixed
+// ≈14 us (tools/pcie_bench: back-to-back 1 MiB H2D at 32 GB/s, 512 MiB at
+// 57), so a batch of objects that lie back to back in host memory (Split
+// images of one arena) moves its small ones — images up to kGroupObjMax — as
+// one copy of their whole images, each then coded in place in the slot;
+// written rows go back per object.  Config 5's trace: 42.47-42.64 -> 43.10-
+// 43.14 GiB/s end to end (profiles/r05_trace_group/, same box, interleaved).
 constexpr size_t kGroupObjMax = (size_t)4 << 20;
+constexpr size_t kGroupDefault = (size_t)16 << 20;
 size_t group_bytes() {
     static const size_t v = [] {
         const char *e = std::getenv("RSGPU_PIPE_GROUP");
-        const long long b = e ? std::atoll(e) : 0;
+        if (!e) return kGroupDefault;
+        const long long b = std::atoll(e);
         return b > 0 ? (size_t)b : (size_t)0;
     }();
     return v;
