@@ -68,23 +68,32 @@ size_t group_bytes() {
     return v;
 }
 
-// [i, end) of `piped`: objects adjacent in host memory (image o+1 starts
-// where image o ends), each image at most kGroupObjMax, the span at most
-// group_bytes(); a single object when grouping is off.  img(o) / base(o):
-// an object's image bytes and first byte.
+// `piped` cut into groups [begin, end): objects adjacent in host memory
+// (image o+1 starts where image o ends), each image at most kGroupObjMax,
+// the span at most group_bytes(); single objects otherwise.  img(o) /
+// base(o): an object's image bytes and first byte.  *slot_bytes grows to hold
+// every group's span (+16 readable bytes).
+struct Group {
+    size_t begin, end, span;
+};
 template <class Img, class Base>
-size_t group_end(const std::vector<int> &piped, size_t i, Img img, Base base, size_t *span) {
-    size_t j = i + 1, sp = img(piped[i]);
+std::vector<Group> make_groups(const std::vector<int> &piped, Img img, Base base, size_t *slot_bytes) {
+    std::vector<Group> out;
     const size_t G = group_bytes();
-    if (G && sp <= kGroupObjMax)
-        while (j < piped.size()) {
-            const int a = piped[j - 1], b = piped[j];
-            if (img(b) > kGroupObjMax || sp + img(b) > G || base(b) != base(a) + img(a)) break;
-            sp += img(b);
-            ++j;
-        }
-    *span = sp;
-    return j;
+    for (size_t i = 0; i < piped.size();) {
+        size_t j = i + 1, sp = G ? img(piped[i]) : 0;
+        if (G && sp <= kGroupObjMax)
+            while (j < piped.size()) {
+                const int a = piped[j - 1], b = piped[j];
+                if (img(b) > kGroupObjMax || sp + img(b) > G || base(b) != base(a) + img(a)) break;
+                sp += img(b);
+                ++j;
+            }
+        if (j - i > 1) *slot_bytes = std::max(*slot_bytes, sp + 16);
+        out.push_back({i, j, sp});
+        i = j;
+    }
+    return out;
 }
 
 int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
@@ -302,17 +311,16 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
         if ((e = rsgpu_encode_image(ctx, objs[o], shard_lens[o], n))) return e;
     if (piped.empty()) return RSGPU_OK;
     auto plan = ctx->plan_encode();
-    std::lock_guard<std::mutex> g(ctx->pipe.mu);
-    if (group_bytes()) maxbytes = std::max(maxbytes, group_bytes() + 16);
-    if ((e = ensure_slots(ctx, maxbytes))) return e;
-    hipError_t he = hipSuccess;
     auto img = [&](int o) { return (size_t)n * shard_lens[o]; };
     auto base = [&](int o) { return (const uint8_t *)objs[o]; };
-    size_t sq = 0;
-    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++sq) {
-        size_t span = 0;
-        const size_t qe = group_end(piped, q, img, base, &span);
-        PipeSlot &s = *ctx->pipe.slots[sq % pipe_slots()];
+    const std::vector<Group> groups = make_groups(piped, img, base, &maxbytes);
+    std::lock_guard<std::mutex> g(ctx->pipe.mu);
+    if ((e = ensure_slots(ctx, maxbytes))) return e;
+    hipError_t he = hipSuccess;
+    for (size_t gi = 0; gi < groups.size() && he == hipSuccess; ++gi) {
+        size_t q = groups[gi].begin;
+        const size_t qe = groups[gi].end, span = groups[gi].span;
+        PipeSlot &s = *ctx->pipe.slots[gi % pipe_slots()];
         // one object: its k data rows; a group: the whole images
         he = hipMemcpyAsync(s.d, objs[piped[q]], qe - q > 1 ? span : (size_t)k * shard_lens[piped[q]],
                             hipMemcpyHostToDevice, s.stream);
@@ -327,7 +335,6 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
                                     hipMemcpyDeviceToHost, s.stream);
             off += (size_t)n * S;
         }
-        q = qe;
     }
     e = drain(ctx);
     if (he != hipSuccess) return hip_fail(he, "rsgpu_encode_batch");
@@ -396,11 +403,6 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
         if ((e = rsgpu_decode(ctx, shards + (size_t)o * n, lens.data(), n, &ok[o]))) return e;
     }
     if (piped.empty()) return RSGPU_OK;
-    std::lock_guard<std::mutex> g(ctx->pipe.mu);
-    if (group_bytes()) maxbytes = std::max(maxbytes, group_bytes() + 16);
-    if ((e = ensure_slots(ctx, maxbytes))) return e;
-    if ((e = ensure_flags(ctx, nobj))) return e;
-    hipError_t he = hipSuccess;
     // grouping (RSGPU_PIPE_GROUP): objects whose shards form one Split image
     // each, back to back in host memory, and whose plans have no check rows
     // (a Get of exactly k bodies); the group's H2D carries every row, the
@@ -415,11 +417,15 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
         return group_bytes() && split_image(o) ? (size_t)n * shard_lens[o] : std::numeric_limits<size_t>::max();
     };
     auto base = [&](int o) { return (const uint8_t *)shards[(size_t)o * n]; };
-    size_t sq = 0;
-    for (size_t q = 0; q < piped.size() && he == hipSuccess; ++sq) {
-        size_t span = 0;
-        const size_t qe = group_end(piped, q, img, base, &span);
-        PipeSlot &s = *ctx->pipe.slots[sq % pipe_slots()];
+    const std::vector<Group> groups = make_groups(piped, img, base, &maxbytes);
+    std::lock_guard<std::mutex> g(ctx->pipe.mu);
+    if ((e = ensure_slots(ctx, maxbytes))) return e;
+    if ((e = ensure_flags(ctx, nobj))) return e;
+    hipError_t he = hipSuccess;
+    for (size_t gi = 0; gi < groups.size() && he == hipSuccess; ++gi) {
+        size_t q = groups[gi].begin;
+        const size_t qe = groups[gi].end, span = groups[gi].span;
+        PipeSlot &s = *ctx->pipe.slots[gi % pipe_slots()];
         if (qe - q > 1) {
             he = hipMemcpyAsync(s.d, base(piped[q]), span, hipMemcpyHostToDevice, s.stream);
             for (size_t off = 0; q < qe && he == hipSuccess; ++q) {
