@@ -487,6 +487,12 @@ class RSEncoder:
         """Encode many objects, each given as its Split() result (or the
         backing array of one): parity rows are written in place.  Host
         buffers from host_alloc()/host_register() make the copies async."""
+        if _pyshards is not None and self._ctx:
+            r = _pyshards.encode_batch(_fn_addr(self._L, "rsgpu_encode_batch"), self._ctx.value or 0, objs,
+                                       self.Shards)
+            if r is not None:
+                _check(r)
+                return
         bases, lens, keep = [], [], []
         for o in objs:
             if isinstance(o, (list, tuple)):
@@ -519,6 +525,12 @@ class RSEncoder:
         filled in place.  With ``present`` (nobj x (k+p) flags) every entry is
         a buffer and the flags say which ones arrived (no allocation).
         Returns the per-object Verify-after-Reconstruct."""
+        if present is not None and _pyshards is not None and self._ctx:
+            r = _pyshards.decode_batch(_fn_addr(self._L, "rsgpu_decode_batch"), self._ctx.value or 0, objs,
+                                       present, self.Shards)
+            if r is not None:
+                _check(r[0])
+                return r[1]
         nobj = len(objs)
         n = self.Shards
         ptrs = (_lib.u8p * (nobj * n))()

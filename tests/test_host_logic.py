@@ -138,3 +138,60 @@ def test_c_marshalling_matches_ctypes_path(monkeypatch):
         assert fast["encode ok"] == ("raise", "NoDevice")
         assert fast["encode 11 shards"] == ("raise", "ErrTooFewShards")
         assert fast["encode read-only parity"] == ("raise", "InvalidArgument")
+
+
+def test_c_batch_marshalling_matches_ctypes_path(monkeypatch):
+    """encode_batch / decode_batch(present=...) marshal in C as well; every
+    argument case ends exactly as through the ctypes tables."""
+    from infinicache_amd import ec
+    assert ec._pyshards is not None
+    k, p = 10, 2
+    n = k + p
+
+    def arena(sizes):
+        Ss = [(nb + k - 1) // k for nb in sizes]
+        buf = np.zeros(sum(n * S for S in Ss), np.uint8)
+        out, off = [], 0
+        for S in Ss:
+            out.append([buf[off + i * S:off + (i + 1) * S] for i in range(n)])
+            off += n * S
+        return out
+
+    def swapped():
+        objs = arena([1000, 2000])
+        objs[1][3], objs[1][4] = objs[1][4], objs[1][3]  # not one Split array
+        return objs
+
+    def readonly():
+        objs = arena([1000])
+        objs[0][11] = np.frombuffer(bytes(len(objs[0][11])), np.uint8)
+        return objs
+
+    pres = lambda nobj, lost=(0, 5): [[i not in lost for i in range(n)]] * nobj  # noqa: E731
+    cases = {
+        "enc lists": lambda e: e.encode_batch(arena([1000, 4096, 7])),
+        "enc arrays": lambda e: e.encode_batch([np.zeros(n * 100, np.uint8), np.zeros(n * 3, np.uint8)]),
+        "enc array not multiple": lambda e: e.encode_batch([np.zeros(n * 100 + 1, np.uint8)]),
+        "enc 11 rows": lambda e: e.encode_batch([arena([1000])[0][:11]]),
+        "enc rows swapped": lambda e: e.encode_batch(swapped()),
+        "enc read-only row": lambda e: e.encode_batch(readonly()),
+        "enc empty": lambda e: e.encode_batch([]),
+        "enc zero-length": lambda e: e.encode_batch([np.zeros(0, np.uint8)]),
+        "dec ok": lambda e: e.decode_batch(arena([1000, 4096]), present=pres(2)),
+        "dec size mismatch": lambda e: e.decode_batch([arena([1000])[0][:11] + [np.zeros(7, np.uint8)]],
+                                                      present=pres(1)),
+        "dec None entry": lambda e: e.decode_batch([[None] + arena([1000])[0][1:]], present=pres(1)),
+        "dec 11 shards": lambda e: e.decode_batch([arena([1000])[0][:11]], present=pres(1)),
+        "dec read-only output": lambda e: e.decode_batch(readonly(), present=pres(1, lost=(11,))),
+        "dec too few present": lambda e: e.decode_batch(arena([1000]), present=pres(1, lost=(0, 1, 2))),
+        "dec empty": lambda e: e.decode_batch([], present=[]),
+    }
+    enc = ia.New(k, p)
+    fast = {name: _outcome(lambda: f(enc)) for name, f in cases.items()}
+    monkeypatch.setattr(ec, "_pyshards", None)
+    slow = {name: _outcome(lambda: f(enc)) for name, f in cases.items()}
+    assert fast == slow
+    if not ia.device_ok(0):
+        assert fast["enc lists"] == ("raise", "NoDevice")
+        assert fast["enc rows swapped"] == ("raise", "InvalidArgument")
+        assert fast["dec size mismatch"] == ("raise", "ErrShardSize")
