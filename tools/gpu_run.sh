@@ -98,6 +98,11 @@ PY
                 RSGPU_PIPE_GROUP=$g run trace_group_${g}_$rep 600 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu
               done
             done ;;
+    trace_marshal) # config 5 with the batch marshalling in C (default) vs ctypes, interleaved
+            for rep in 1 2; do
+              run trace_c_$rep 600 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu
+              INFINICACHE_PY_MARSHAL=ctypes run trace_ctypes_$rep 600 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu
+            done ;;
     tests)  # a chosen set of GPU test files (TESTS), one pytest process
             run pytest_sel 900 python -u -m pytest ${TESTS} -m gpu -x -v -s --timeout 150 --timeout-method thread ;;
     rccl1)  # BASELINE config 4's collectives over RCCL with one rank (the -m gpu test writes the line)
