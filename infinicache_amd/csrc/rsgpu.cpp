@@ -276,12 +276,12 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         L.out_base = s->hdev;
         L.out_dual = then != nullptr;
     }
-    // Copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent>): a
-    // pass reading host memory moves ~36 GB/s, a DMA ~55 GB/s
-    // (profiles/r04_redirect_bs_sweep.txt, r01_pcie_bench.txt), so the input
-    // rows' last columns [cb, size) go H2D on a second stream and a second
-    // pass codes them from HBM while the first pass codes columns [0, cb)
-    // over PCIe.  Every operation is a byte-column map.  The second share is
+    // Copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent>; a
+    // measurement, off by default): the input rows' last columns [cb, size)
+    // go H2D on a second stream and a second pass codes them from HBM while
+    // the first pass codes columns [0, cb) over PCIe.  Measured 4x slower at
+    // 1 MiB — each row slice's copy command carries a fixed ~10-14 us — and
+    // not kept (profiles/r05_dma_split_not_kept/).  Every operation is a byte-column map.  The second share is
     // whole 16-B vectors, so its last vector ends at the row's end; the first
     // share's last vector may reach into the second's first vector, where
     // both passes store the same bytes (the coding of the same input
