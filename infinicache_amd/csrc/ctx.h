@@ -424,8 +424,8 @@ struct rsgpu_ctx {
             HIP_TRY(hipHostGetDevicePointer((void **)&s->m_bad, s->h_bad, 0));
         }
         if (s->cap < bytes) {
-            // the old images are retired (freed at once unless a worker runs);
-            // growth at least 1.5x bounds what a running worker keeps
+            // the old images are retired (freed at once unless a worker kernel
+            // is resident, devmem.cpp); growth at least 1.5x
             retire(s->h, true, s->cap);
             retire(s->d, false, s->cap);
             const size_t cap = round_up(std::max(bytes, s->cap + s->cap / 2), (size_t)1 << 20);

@@ -132,7 +132,7 @@ hipError_t StatusScratch::acquire(size_t nobj, hipStream_t stream, Slot *&s) {
     else e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
     if (e == hipSuccess && s->cap < nobj) {
         const size_t cap = std::max<size_t>({nobj, 1024, s->cap * 2});
-        retire(s->d, false);  // (freed once no worker runs: devmem.cpp)
+        retire(s->d, false);  // (held while a worker kernel is resident: devmem.cpp)
         s->d = nullptr;
         s->cap = 0;
         e = hipMalloc(&s->d, cap * 2 * sizeof(uint32_t));
