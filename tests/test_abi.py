@@ -278,3 +278,13 @@ def test_copy_pieces_argument_checks():
     if not ia.device_ok(0):
         with pytest.raises(ia.NoDevice):
             enc.copy_pieces(0x1000, 1200, 12 * 1200, 0x100000, 4096, 128, 100, 4)
+
+
+def test_diagnostics_and_knobs_without_device():
+    """rsgpu_retired_stats / rsgpu_set_slab_bytes need no device: nothing is
+    held back in a process that never started a worker, and the slab size
+    setter accepts any value (< 4096 restores the 1 GiB default)."""
+    st = ia.retired_stats()
+    assert st == {"count": 0, "bytes": 0, "deferred": 0}
+    for v in (0, 1, 4095, 4096, 1 << 20, 0):
+        ia.set_slab_bytes(v)
