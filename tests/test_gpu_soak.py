@@ -23,7 +23,9 @@ than tests/test_gpu_random.py:
     slices over several mailboxes, shards up to 64 KiB) and host ops coded in
     column slabs (RSGPU_SLAB_BYTES drawn small, so objects of a few KB take
     several slabs), and pageable objects of 13-20 MB whose staging copies
-    run on the host copy pool.
+    run on the host copy pool;
+  * round 5: the host batch pipeline over random arenas (adjacent small
+    objects in one H2D), pinned and pageable, with per-object Get patterns.
 Every result is compared bit-exact (bytes) or exactly (booleans, error
 classes) with the oracle on the same input.  Prints a per-kind case count."""
 import collections
@@ -536,6 +538,74 @@ def _slab_case(rng, counts):
         ia.set_slab_bytes(0)
 
 
+def _batch_case(rng, counts):
+    """round 5: the host batch pipeline (rsgpu_encode_batch / _decode_batch):
+    1-14 objects of 1 B - 700 KB (now and then one past the 4 MiB group
+    limit), Split images back to back in one arena with random gaps (runs of
+    adjacent small objects move as one H2D), pinned or pageable; encode vs
+    the oracle, then a Get per object with its own present pattern (exactly
+    k bodies, or extra bodies with a corrupted one: coded alone, flagged)."""
+    k = int(rng.integers(1, 17))
+    p = int(rng.integers(1, 5))
+    n = k + p
+    kind = str(rng.choice(["vandermonde", "cauchy"]))
+    enc = ia.New(k, p, matrix=kind)
+    nobj = int(rng.integers(1, 15))
+    sizes = [_size(rng, 700000) for _ in range(nobj)]
+    if rng.random() < 0.1:
+        sizes[int(rng.integers(0, nobj))] = int(rng.integers(4 << 20, 6 << 20))
+    Ss = [(nb + k - 1) // k for nb in sizes]
+    gaps = [int(rng.choice([0, 0, 0, 16, 4096])) for _ in range(nobj)]
+    total = sum(n * S + g for S, g in zip(Ss, gaps))
+    pinned = rng.random() < 0.5
+    arena = ia.host_alloc(total) if pinned else np.empty(total, np.uint8)
+    objs, fulls, off = [], [], 0
+    for S, g in zip(Ss, gaps):
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+        e, full = oracle.encode(k, p, data + [bytes(S)] * p, kind)
+        assert e == 0
+        img = arena[off:off + n * S]
+        for i in range(k):
+            img[i * S:(i + 1) * S] = full[i]
+        img[k * S:] = 0x3C
+        objs.append([img[i * S:(i + 1) * S] for i in range(n)])
+        fulls.append(full)
+        off += n * S + g
+    tag = ("batch", k, p, kind, nobj, sizes, gaps, pinned)
+    enc.encode_batch(objs)
+    for o in range(nobj):
+        for i in range(k, n):
+            assert np.array_equal(objs[o][i], fulls[o][i]), (tag, o, i)
+    present, want_ok = [], []
+    for o in range(nobj):
+        nlost = int(rng.integers(0, p + 1))
+        lost = set(rng.choice(n, nlost, replace=False).tolist())
+        pr = [i not in lost for i in range(n)]
+        for i in lost:
+            objs[o][i][:] = 0xA5
+        ok = True
+        extra = [i for i in range(n) if pr[i]][k:]
+        if extra and rng.random() < 0.3:  # a corrupted body beyond the survivors
+            j = extra[int(rng.integers(0, len(extra)))]
+            objs[o][j][int(rng.integers(0, Ss[o]))] ^= 0x5A
+            ok = j < k  # upstream Verify compares parity rows only
+        present.append(pr)
+        want_ok.append(ok)
+    counts["batch_" + ("pinned" if pinned else "pageable")] += 1
+    got = enc.decode_batch(objs, present=present)
+    for o in range(nobj):
+        if not want_ok[o] or got[o] != want_ok[o]:
+            # the oracle decides (a corrupted data extra still verifies)
+            ref = [objs[o][i].copy() if present[o][i] else None for i in range(n)]
+            e, rec = oracle.reconstruct(k, p, ref, kind)
+            assert e == 0
+            e, v = oracle.verify(k, p, rec, kind)
+            assert e == 0 and got[o] == v, (tag, o)
+        for i in range(n):
+            if not present[o][i]:
+                assert np.array_equal(objs[o][i], fulls[o][i]), (tag, o, i)
+
+
 def test_gpu_soak_vs_oracle(gpu):
     seed = int(os.environ.get("RSGPU_SOAK_SEED", "20261016"))
     rng = np.random.default_rng(seed)
@@ -557,8 +627,10 @@ def test_gpu_soak_vs_oracle(gpu):
             _worker_case(rng, counts)
         elif r < 0.94:
             _objs_case(rng, counts)
-        elif r < 0.99:
+        elif r < 0.96:
             _slab_case(rng, counts)
+        elif r < 0.99:
+            _batch_case(rng, counts)
         else:
             _large_pageable_case(rng, counts)
         if time.time() - last > 30:  # progress line (a silent GPU run reads as hung)
