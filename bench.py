@@ -121,6 +121,23 @@ WORKLOADS = {
                  ops=("decode",), data_only=True,
                  desc="RS(10+4) ReconstructData, data shards {0,5} missing (10 of 14 present), "
                       "4 MiB objects, batch 512/GPU"),
+    # BASELINE config 3 as the reference's Client.decode runs it
+    # (client/ecRedis.go:404-427): with 2 data shards lost, 12 of 14 shards
+    # are present, so the Get rebuilds {0,5} from the first 10 present and
+    # verifies the whole object, which checks the 2 extra parity shards
+    #   dec4_get:      one fused launch: 12 rows in, 2 rows written, 2 parity
+    #                  rows checked in registers (rsgpu_decode_dev)
+    #   dec4_upstream: upstream's passes as they are: Reconstruct (10 rows in,
+    #                  2 written), then a full Verify (14 rows in, 4 checked)
+    "dec4_get": dict(k=10, p=4, nbytes=4 << 20, batch=512, lost=(0, 5), ops=("decode",),
+                     desc="RS(10+4) Get as Client.decode runs it: 12 of 14 shards present, data {0,5} "
+                          "rebuilt from the first 10 and the 2 extra parity shards verified, fused in one "
+                          "pass, 4 MiB objects, batch 512/GPU"),
+    "dec4_upstream": dict(k=10, p=4, nbytes=4 << 20, batch=512, lost=(0, 5), ops=("decode",),
+                          upstream_get=True,
+                          desc="RS(10+4) Get as Client.decode runs it, unfused: Reconstruct of data {0,5} "
+                               "from the first 10 of 12 present shards, then a separate full Verify pass "
+                               "over all 14 rows, 4 MiB objects, batch 512/GPU"),
 }
 METRICS = {
     "encdec": "RS(10+2) encode+decode GiB/s (device-resident), 1 MB objects, 1/2/4/8 GPU",
@@ -143,6 +160,10 @@ METRICS = {
     "small_p64": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
     "small_p128": "RS(10+2) encode+decode GiB/s (device-resident), 4 KiB objects",
     "dec4": "RS(10+4) decode (2 missing data shards) GiB/s, 4 MB objects",
+    "dec4_get": "RS(10+4) decode (2 missing data shards, Client.decode Reconstruct+Verify fused) GiB/s, "
+                "4 MB objects",
+    "dec4_upstream": "RS(10+4) decode (2 missing data shards, Client.decode Reconstruct then Verify, "
+                     "unfused) GiB/s, 4 MB objects",
 }
 
 
@@ -150,7 +171,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, windows=3):
+def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, windows=3, fused_checks=0):
     """Time the oracle's port of the Go path (upstream galMulAVX2Xor /
     codeSomeShardsAvx512 SIMD coders) over a bounded sample laid out like the
     GPU batch, bit-compare with the GPU output.  Headline form: object-
@@ -158,33 +179,58 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
     run) on `threads` threads (the box's cgroup share) and on 1 thread, each
     the MEDIAN of `windows` timing windows (SURVEY §8d: 1-core and all-core);
     the per-object codeSomeShardsP split form (maxGoroutines 32, minSplitSize
-    1024, client/example/main.go:22) is timed beside it for reference."""
+    1024, client/example/main.go:22) is timed beside it for reference.
+
+    A decode that verifies (the Get of dec4_get / *_upstream: 12 of 14 shards
+    present, or upstream's separate Verify) is timed the way the Go path runs
+    it: Reconstruct, then Verify re-encoding every parity row from the data
+    rows and comparing (client/ecRedis.go:414-420); with fused_checks > 0 the
+    fused form (the extra shards checked from the survivors in the decode's
+    own pass) is timed beside it."""
     import ctypes
 
     import oracle
+    from oracle import rs_numpy as rn
     k, p = w["k"], w["p"]
     n = k + p
     S = (w["nbytes"] + k - 1) // k
     ns, _, pitch = sample.shape
     lost = list(w["lost"])
-    surv = [i for i in range(n) if i not in lost and i not in w.get("absent", ())][:k]
+    present = [i for i in range(n) if i not in lost and i not in w.get("absent", ())]
+    surv = present[:k]
     base = sample.reshape(-1)
+    verifies = "decode" in w["ops"] and (w.get("upstream_get") or fused_checks > 0)
+    extras = present[k:]
+    fused_coef = None
+    if fused_checks > 0:  # check rows of the extra shards, over the survivors
+        fused_coef = np.concatenate([inv_rows, rn.matmul(m[extras], rn.invert(m[surv]))])
+    verified = [True]
 
-    def one_pass(nt, nobj):
+    def one_pass(nt, nobj, form="upstream"):
         if "encode" in w["ops"]:
             oracle.code_batch(m[k:], list(range(k)), list(range(k, n)), base, n * pitch, pitch, S,
                               nobj, nthreads=nt)
         if "decode" in w["ops"]:
+            if form == "fused":  # rebuilt rows written, extra shards compared, one pass per object
+                oracle.code_batch(inv_rows, surv, lost, base, n * pitch, pitch, S, nobj, nthreads=nt)
+                ok = oracle.verify_batch(fused_coef[len(lost):], surv, extras, base, n * pitch, pitch, S,
+                                         nobj, nthreads=nt)
+                verified[0] &= bool(ok.all())
+                return
             oracle.code_batch(inv_rows, surv, lost, base, n * pitch, pitch, S, nobj, nthreads=nt)
+            if verifies:  # upstream Verify: all parity re-encoded from the data rows, compared
+                ok = oracle.verify_batch(m[k:], list(range(k)), list(range(k, n)), base, n * pitch, pitch,
+                                         S, nobj, nthreads=nt)
+                verified[0] &= bool(ok.all())
 
-    def rate(nt, nobj, secs):
+    def rate(nt, nobj, secs, form="upstream"):
         """median GiB/s over `windows` windows of ~secs each"""
-        one_pass(nt, nobj)  # warm the pool and the pages
+        one_pass(nt, nobj, form)  # warm the pool and the pages
         vals = []
         for _ in range(windows):
             reps, t0 = 0, time.perf_counter()
             while True:
-                one_pass(nt, nobj)
+                one_pass(nt, nobj, form)
                 reps += 1
                 el = time.perf_counter() - t0
                 if el >= secs:
@@ -194,7 +240,10 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
 
     all_v, all_w = rate(threads, ns, budget_s * 0.5 / windows)
     one_v, one_w = rate(1, ns, budget_s * 0.3 / windows)  # same sample: beyond the host's L3
-    exact = bool(np.array_equal(sample[:, :, :S], gpu_sample[:, :, :S]))
+    fused_v = None
+    if fused_coef is not None:
+        fused_v, _ = rate(threads, ns, budget_s * 0.2 / windows, form="fused")
+    exact = bool(np.array_equal(sample[:, :, :S], gpu_sample[:, :, :S])) and verified[0]
     if "encode" in w["ops"] and "decode" in w["ops"]:
         # the encode pass above needs the data rows, so the rows the GPU
         # rebuilt are checked by a separate CPU decode: erase them again and
@@ -213,6 +262,9 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
             if "decode" in w["ops"]:
                 oracle.code_fast(inv_rows, [sample[o, c, :S] for c in surv], nthreads=threads,
                                  max_goroutines=32)
+                if verifies:
+                    oracle.code_fast(m[k:], [sample[o, c, :S] for c in range(k)], nthreads=threads,
+                                     max_goroutines=32)
         sreps += 1
     split_val = ns * sreps * w["nbytes"] * len(w["ops"]) / (time.perf_counter() - t1) / GiB
     # the host's one-thread memory rate beside it: the 1-core coder figure
@@ -243,6 +295,8 @@ def cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=10.0, threads=16, 
         "windows_GiBps": [round(v, 2) for v in all_w],
         "one_core": {"value": round(one_v, 3), "cores": 1, "windows_GiBps": [round(v, 2) for v in one_w]},
         "per_object_split_form_GiBps": round(split_val, 3),
+        **({"decode_form": "Reconstruct then Verify of all parity rows (the Go path, client/ecRedis.go:414-420)",
+            "fused_form_GiBps": round(fused_v, 3) if fused_v is not None else None} if verifies else {}),
         "host_copy_GBps_1thread": round(copy_gbps, 1),
         "sample": f"{ns} x {w['nbytes'] >> 10} KiB objects ({' + '.join(w['ops'])}), object-parallel; value = "
                   f"median of {windows} windows on {threads} threads (the box's cgroup share), one_core = "
@@ -464,6 +518,33 @@ def run_trace(args):
     present = [[i not in lost for i in range(n)]] * nobj
     golden = [[objs[o][i].copy() for i in lost] for o in range(0, nobj, 37)]
 
+    # the link's own rate, measured in this process before the timed region:
+    # one pinned 1D copy of 512 MiB per direction (best of 5), the same kind
+    # of memory the trace's objects live in (hipHostMalloc'd), GPU 0
+    def link_rate(h2d):
+        nb = 512 << 20
+        hbuf = ia.host_alloc(nb)
+        hbuf[:] = 1
+        ht = torch.from_numpy(hbuf)
+        dt = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        best = 0.0
+        for _ in range(6):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            if h2d:
+                dt.copy_(ht, non_blocking=True)
+            else:
+                ht.copy_(dt, non_blocking=True)
+            torch.cuda.synchronize()
+            best = max(best, nb / (time.perf_counter() - t) / 1e9)
+        del ht, dt, hbuf
+        return best
+    link_h2d_gbs, link_d2h_gbs = link_rate(True), link_rate(False)
+    # bytes each step moves over the link (encode_batch: data rows in, parity
+    # out; decode_batch: the first k present rows in, the 2 rebuilt rows out)
+    h2d_step = int(sum(2 * k * int(x) for x in S))
+    d2h_step = int(sum((p + len(lost)) * int(x) for x in S))
+
     def step():
         enc.encode_batch(objs)
         oks = enc.decode_batch(objs, present=present)
@@ -480,6 +561,8 @@ def run_trace(args):
         for g, i in zip(golden[j], lost):
             assert np.array_equal(objs[o][i], g), "decode did not restore the data rows"
     e2e = 2 * total_obj * args.steps / el / GiB
+    h2d_gbs = h2d_step * args.steps / el / 1e9
+    d2h_gbs = d2h_step * args.steps / el / 1e9
 
     # the same trace device-resident (kernel + launch only, no PCIe)
     pitches = [(int(x) + 255) // 256 * 256 for x in S]
@@ -579,6 +662,27 @@ def run_trace(args):
         "device_resident_check": dev_check,
         "device_resident_per_object_launches_GiBps": round(per_obj_rate, 2),
         "kernel_fraction_of_e2e_time": round(dev_el / el, 4),
+        # the e2e path is bound by the PCIe link's host-to-device direction:
+        # achieved = H2D bytes the step moves / step time, peak = the pinned
+        # 1D H2D copy rate measured in this process before the timed region
+        # (D2H runs concurrently on the other direction of the link)
+        "roofline": {
+            "bound": "pcie-h2d",
+            "achieved": round(h2d_gbs, 2),
+            "peak": round(link_h2d_gbs, 2),
+            "unit": "GB/s",
+            "frac": round(h2d_gbs / link_h2d_gbs, 4),
+            "traffic": h2d_step,
+            "traffic_note": "H2D bytes per step (2 x k x shard_len per object: the encode's data rows and the "
+                            "decode's k survivors); per-step, not per kernel launch",
+            "d2h": {"achieved": round(d2h_gbs, 2), "peak": round(link_d2h_gbs, 2),
+                    "frac": round(d2h_gbs / link_d2h_gbs, 4), "bytes_per_step": d2h_step,
+                    "share_of_link_bytes": round(d2h_step / (h2d_step + d2h_step), 4)},
+            "peak_source": "pinned 1D copy of 512 MiB per direction, hipHostMalloc'd host memory, best of 6, "
+                           "this process, before the timed region",
+        },
+        **({"winner": ("gpu_e2e" if e2e > cpu["value"] else "cpu_port"),
+            "gpu_e2e_over_cpu": round(e2e / cpu["value"], 3)} if cpu else {}),
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
@@ -817,6 +921,34 @@ def main():
 
     op_fns = {"encode": op_encode, "decode": op_decode}
 
+    # timing units: each op, except the unfused upstream Get, which is timed
+    # (and profiled) as its two launches
+    def op_reconstruct(buf, cnt=None):
+        enc.reconstruct_dev(buf, present, S, pitch, stride, nobj if cnt is None else cnt, data_only=False,
+                            stream=stream)
+
+    def op_verify(buf, cnt=None):
+        enc.verify_dev(buf, S, pitch, stride, nobj if cnt is None else cnt, bad, stream)
+
+    units = []
+    for op in w["ops"]:
+        if op == "decode" and w.get("upstream_get"):
+            units += [("decode:reconstruct", op_reconstruct), ("decode:verify", op_verify)]
+        else:
+            units.append((op, op_fns[op]))
+
+    # rows of the decode: present shards, rows it writes, and the extra present
+    # shards (beyond the first k) the fused Get checks in the same pass
+    n_present = sum(present)
+    e_rows = len(w["lost"]) + (0 if w.get("data_only") else len(w.get("absent", ())))
+    fused_checks = 0 if (w.get("data_only") or w.get("upstream_get") or w.get("mixed")) else n_present - k
+    # the row the corruption check flips: a present parity row that the decode
+    # verifies (fused: an extra shard; upstream: Verify reads every row)
+    check_row = None
+    if "decode" in w["ops"] and (fused_checks > 0 or (w.get("upstream_get") and n_present > k)) \
+            and not w.get("shard_major"):
+        check_row = max(i for i in range(n) if present[i])
+
     # rows each op writes, per (object, shard row)
     written = {}
     if "encode" in w["ops"]:
@@ -864,6 +996,26 @@ def main():
                 raise SystemExit(f"{op} check FAILED: rewritten rows differ from the rows before")
             out[op] = {"result": "bit-exact", "objects": nobj, "rows_rewritten": int(E.sum()),
                        "bytes_compared": int(E.sum()) * S}
+            if op == "decode" and check_row is not None:
+                # one corrupted byte in a checked parity row of one object:
+                # the decode must flag exactly that object (and still rebuild
+                # every object's lost rows bit-exact)
+                o = nobj // 2
+                buf[o, check_row, S - 1] ^= 0x5A
+                ref = buf.clone()
+                buf[E] = 0
+                bad.fill_(7)
+                op_fns[op](buf)
+                torch.cuda.synchronize(dev)
+                flagged = torch.nonzero(bad).flatten().tolist()
+                same = torch.equal(buf[..., :S], ref[..., :S])
+                buf[o, check_row, S - 1] ^= 0x5A
+                del ref
+                if flagged != [o] or not same:
+                    raise SystemExit(f"{op} corruption check FAILED: flagged {flagged[:8]}, expected [{o}]; "
+                                     f"rebuilt rows {'equal' if same else 'DIFFER'}")
+                out[op]["corruption_check"] = {"object": o, "row": check_row, "byte": S - 1,
+                                               "flagged": flagged, "result": "exactly that object flagged"}
         return out
 
     turn = [0]
@@ -881,15 +1033,15 @@ def main():
         so the average is the kernel's own time plus launch gaps; the timed
         steps above carry no events at all."""
         out = {}
-        for op in w["ops"]:
+        for name, fn in units:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            op_fns[op](bufs[0 if fixed is not None else 1 % copies])  # untimed: same launch shape warm
+            fn(bufs[0 if fixed is not None else 1 % copies])  # untimed: same launch shape warm
             e0.record(stream)
             for i in range(args.steps):
-                op_fns[op](bufs[fixed if fixed is not None else i % copies])
+                fn(bufs[fixed if fixed is not None else i % copies])
             e1.record(stream)
             e1.synchronize()
-            out[op] = e0.elapsed_time(e1) / args.steps
+            out[name] = e0.elapsed_time(e1) / args.steps
         return out
 
     dctx = DistCtx(world, rank, dev, force=force_coll)
@@ -936,6 +1088,9 @@ def main():
     # erased rows) with random garbage, run the op, and compare the rows'
     # shard_len bytes with a copy taken before (client/ecRedis.go:390,404-427).
     work_check = check_ops(bufs[0])
+    # every rank's own check passed (a failing rank exits before this point):
+    # 1 per rank, in rank order
+    wc_ranks = [int(round(x)) for x in dctx.gather(1.0)]
     kms_alone = kernel_ms()
     # Each op's share of the timed step comes from its uninterrupted run; run
     # alone an op can be a little slower than inside the step (there a decode
@@ -945,7 +1100,6 @@ def main():
     ms_per_step_meas = elapsed / args.steps * 1e3
     scale = min(1.0, ms_per_step_meas / max(sum(kms_alone.values()), 1e-9))
     kms = {op: t * scale for op, t in kms_alone.items()}
-    enc_ms, dec_ms = kms.get("encode", 0.0), kms.get("decode", 0.0)
     ops = len(w["ops"])
 
     # --warm: the same K steps on ONE batch (warm Infinity Cache), for
@@ -962,36 +1116,34 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # algorithmic bytes per launch: encode k*S read + p*S write;
-    # decode (e missing data rows) k*S read + e*S write; on unpadded S
-    # a Get's decode rebuilds every missing row, parity included (upstream
-    # Reconstruct, ecRedis.go:415), unless the workload is ReconstructData
-    e_rows = len(w["lost"]) + (0 if w.get("data_only") else len(w.get("absent", ())))
-    enc_bytes = nobj * (k + p) * S
-    dec_bytes = nobj * (k + e_rows) * S
-    if w.get("upstream_get"):  # + Verify: reads all k+p rows again
-        dec_bytes += nobj * (k + p) * S
-    # launches grouped by kernel symbol: encode and the uniform-pattern decode
-    # of RS(10+2) are the same kernel (gf_apply_kernel<10,2>) with the same
-    # algorithmic bytes per launch, so its average duration is over both, as
-    # rocprofv3 --stats reports it
+    # decode: every row it reads (the first k present, plus the extra present
+    # shards a fused Get checks) + every row it writes (each missing row, parity
+    # included (upstream Reconstruct, ecRedis.go:415), unless ReconstructData);
+    # upstream's separate Verify reads all k+p rows
+    dec_in = k + fused_checks
     enc_sym = f"gf_apply_kernel<{k},{p}>"
-    dec_sym = f"gf_apply_kernel<{k},{e_rows}>"
+    dec_sym = f"gf_apply_kernel<{dec_in},{e_rows + fused_checks}>"
     if k > 16:  # generic kernel, one launch per <= 8 rows
         enc_sym, dec_sym = f"gf_apply_generic<{min(p, 8)}>", f"gf_apply_generic<{e_rows}>"
     if w.get("mixed"):  # device-resolved patterns: KMAX = n inputs (gf_masked.h)
         dec_sym = f"gf_apply_{'lanes' if ((S + 15) // 16) * 2 <= 256 else 'masked'}<{n},{min(p, 4)}>"
-    if w.get("upstream_get"):
-        dec_sym = f"gf_apply_kernel<{k},{e_rows}>+gf_apply_kernel<{k + p},{p}>"
-    per_op = {}
-    if "encode" in w["ops"]:
-        per_op["encode"] = (enc_sym, enc_bytes, enc_ms)
-    if "decode" in w["ops"]:
-        per_op["decode"] = (dec_sym, dec_bytes, dec_ms)
+    # unit -> (kernel symbol, algorithmic bytes per launch, bytes read per launch)
+    unit_info = {
+        "encode": (enc_sym, nobj * n * S, nobj * k * S),
+        "decode": (dec_sym, nobj * (dec_in + e_rows) * S, nobj * dec_in * S),
+        "decode:reconstruct": (f"gf_apply_kernel<{k},{e_rows}>", nobj * (k + e_rows) * S, nobj * k * S),
+        "decode:verify": (f"gf_apply_kernel<{n},{p}>", nobj * n * S, nobj * n * S),
+    }
+    # launches grouped by kernel symbol: encode and the uniform-pattern decode
+    # of RS(10+2) are the same kernel (gf_apply_kernel<10,2>) with the same
+    # algorithmic bytes per launch, so its average duration is over both, as
+    # rocprofv3 --stats reports it
+    per_op = {name: (*unit_info[name], kms[name]) for name, _ in units}
     groups = {}
-    for op, (sym, b, ms) in per_op.items():
-        groups.setdefault((sym, b), []).append((op, ms))
+    for op, (sym, b, rb, ms) in per_op.items():
+        groups.setdefault((sym, b, rb), []).append((op, ms))
     # dominant: the kernel with the most time per step
-    (kernel_key, dom_bytes), members = max(groups.items(), key=lambda kv: sum(m for _, m in kv[1]))
+    (kernel_key, dom_bytes, dom_read), members = max(groups.items(), key=lambda kv: sum(m for _, m in kv[1]))
     dom_ms = float(np.mean([m for _, m in members]))
     dom = "+".join(op for op, _ in members)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
@@ -1023,10 +1175,11 @@ def main():
                   f"per op after the timed steps, scaled x{scale:.4f} to the timed step)",
         "kernel_ms_per_step": round(sum(kms.values()), 4),
         "kernel_ms_alone": {op: round(t, 4) for op, t in kms_alone.items()},
-        "per_kernel_GBps": {op: round(b / (ms * 1e-3) / 1e9, 1) for op, (_, b, ms) in per_op.items()},
-        # the read side alone (k*S input bytes per object and launch), SURVEY §8d
-        "read_only": {"achieved": round(nobj * k * S / (dom_ms * 1e-3) / 1e9, 1),
-                      "frac": round(nobj * k * S / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "per_kernel_GBps": {op: round(b / (ms * 1e-3) / 1e9, 1) for op, (_, b, _rb, ms) in per_op.items()},
+        "per_kernel_symbol": {op: sym for op, (sym, _b, _rb, _ms) in per_op.items()},
+        # the read side alone (the input rows per object and launch), SURVEY §8d
+        "read_only": {"achieved": round(dom_read / (dom_ms * 1e-3) / 1e9, 1),
+                      "frac": round(dom_read / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         # achieved / peak of the same kernel on each rank's GPU (rank order);
         # achieved and frac above are rank 0's
         "frac_per_rank": frac_ranks,
@@ -1061,7 +1214,7 @@ def main():
         surv = [i for i in range(n) if present[i]][:k]
         inv_rows = rn.invert(m[surv])[list(w["lost"])] if w["lost"] else None
         cpu = cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=args.cpu_seconds,
-                           threads=int(os.environ.get("BENCH_CPU_THREADS", "16")))
+                           threads=int(os.environ.get("BENCH_CPU_THREADS", "16")), fused_checks=fused_checks)
 
     if rank == 0:
         out = {
@@ -1098,6 +1251,7 @@ def main():
             "roofline": roofline,
             **({"decode_check": work_check["decode"]["result"]} if "decode" in work_check else {}),
             "work_check": work_check,
+            "work_check_ranks": wc_ranks,
             **({"warm_repeat": warm} if warm else {}),
             **({"strong_scaling": strong} if strong else {}),
             **({"collectives_issued": dctx.calls} if dist_on else {}),

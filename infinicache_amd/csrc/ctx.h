@@ -30,15 +30,19 @@ struct Slot {
     uint8_t *hdev = nullptr;  // device address of the pinned staging image h
     size_t cap = 0;
     hipStream_t stream = nullptr;
+#ifdef RSGPU_MEASURE_DMA_SPLIT
     // a second stream (and its event) for the copy-engine share of a split
-    // per-object call (rsgpu.cpp run_host_once, RSGPU_DMA_SPLIT)
+    // per-object call (rsgpu.cpp run_host_once; measurement builds only)
     hipStream_t stream2 = nullptr;
     hipEvent_t ev2 = nullptr;
+#endif
     uint32_t *d_bad = nullptr, *h_bad = nullptr;
     uint32_t *m_bad = nullptr;  // device address of h_bad (mapped pinned memory)
     ~Slot() {
+#ifdef RSGPU_MEASURE_DMA_SPLIT
         if (ev2) (void)hipEventDestroy(ev2);
         if (stream2) (void)hipStreamDestroy(stream2);
+#endif
         if (stream) (void)hipStreamDestroy(stream);
         retire(h, true, cap);
         retire(d, false, cap);

@@ -110,7 +110,7 @@ void retire(void *p, bool host, size_t bytes) {
     free_now(p, host);
 }
 
-int free_user(void *p, bool host) {
+int free_user(void *p, bool host, size_t bytes) {
     Graveyard &g = graveyard();
     {
         std::lock_guard<std::mutex> l(g.mu);
@@ -120,7 +120,7 @@ int free_user(void *p, bool host) {
             return hipFree(p) == hipSuccess ? RSGPU_OK : RSGPU_ERR_HIP;
         }
         if (g.kept_bytes < kKeptCap) {
-            const size_t b = alloc_bytes(p);
+            const size_t b = bytes ? bytes : alloc_bytes(p);
             g.kept.push_back({p, host, b});
             g.kept_bytes += b;
             ++g.deferred;

@@ -18,8 +18,9 @@ void retire(void *p, bool host, size_t bytes = 0);
 // the bound on kept bytes: past it the workers are parked (their kernels
 // leave) and everything kept is freed
 constexpr size_t kKeptCap = (size_t)256 << 20;
-// a user's free (rsgpu_host_free): as retire(), with the bound
-int free_user(void *p, bool host);
+// a user's free (rsgpu_host_free): as retire(), with the bound; bytes: the
+// allocation's size when the caller knows it (0: asked of the runtime)
+int free_user(void *p, bool host, size_t bytes = 0);
 // the bound at the library's own safe points (no library lock held: it may
 // park the workers)
 void relieve_retired();

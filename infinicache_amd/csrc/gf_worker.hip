@@ -856,6 +856,10 @@ void print_trace(Worker &w) {
 // teardown was registered before), so it runs first and stops every worker.
 std::mutex g_live_mu;
 std::set<rsgpu_ctx *> g_live;
+// stops in progress: from before the stopping worker leaves the probe's view
+// (ctx->worker_raw cleared) until its kernel has left (quiesce), the probe
+// counts it as resident
+std::atomic<int> g_stopping{0};
 // parks, starts and stops one at a time (each takes every mailbox of the
 // workers it touches; two of them interleaving would each hold a part)
 std::mutex g_park_mu;
@@ -909,6 +913,7 @@ struct WorkerRef {
 // epoch, so a concurrent stop cannot free it meanwhile (and this never drops
 // the last reference).
 bool workers_resident() {
+    if (g_stopping.load(std::memory_order_seq_cst) > 0) return true;
     std::lock_guard<std::mutex> l(g_live_mu);
     for (rsgpu_ctx *c : g_live) {
         const WorkerRef ref(c);
@@ -920,8 +925,12 @@ bool workers_resident() {
 // ctx's worker stopped and detached (ctx->worker_mu and g_park_mu held)
 int stop_locked(rsgpu_ctx *ctx) {
     std::shared_ptr<Worker> w = std::atomic_exchange(&ctx->worker, std::shared_ptr<Worker>());
+    if (!w) {
+        track_worker(ctx, false);
+        return RSGPU_OK;
+    }
+    g_stopping.fetch_add(1, std::memory_order_seq_cst);  // resident to the probe until quiesce is done
     track_worker(ctx, false);
-    if (!w) return RSGPU_OK;
     // no new call finds it; the calls that may hold it finish (they are
     // declined below, or finish a request they already posted)
     ctx->worker_raw.store(nullptr, std::memory_order_seq_cst);
@@ -930,6 +939,7 @@ int stop_locked(rsgpu_ctx *ctx) {
     DeviceGuard dg_;
     int e = ctx->use_device(dg_, false);
     if (!e) e = quiesce(*w);
+    g_stopping.fetch_sub(1, std::memory_order_seq_cst);
     while (ctx->worker_readers[old].load(std::memory_order_acquire) != 0) std::this_thread::yield();
     if (w->trace) print_trace(*w);
     // its kernel has left: what was retired while it ran may be freed now
@@ -1195,9 +1205,10 @@ int rsgpu_worker_start(rsgpu_ctx *ctx, int nslots, unsigned idle_us, size_t max_
     if ((e = worker_create(ctx, nslots, idle_us, max_shard, w))) return e;
     worker_count(+1);  // before its first launch (the first request's)
     std::shared_ptr<Worker> sp(w.release());
+    // in the probe's view before any caller can find it (and so launch it)
+    track_worker(ctx, true);
     ctx->worker_raw.store(sp.get(), std::memory_order_seq_cst);
     std::atomic_store(&ctx->worker, std::move(sp));
-    track_worker(ctx, true);
     return RSGPU_OK;
 }
 

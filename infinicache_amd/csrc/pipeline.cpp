@@ -96,7 +96,20 @@ std::vector<Group> make_groups(const std::vector<int> &piped, Img img, Base base
     return out;
 }
 
-int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
+// relieve_retired() for a scope, run when it ends: declared before the
+// scope's lock_guard on ctx->pipe.mu, so it runs after the lock is released
+// (relieve_retired may park every worker: no library lock may be held,
+// devmem.h)
+struct RelieveAfter {
+    bool on = false;
+    ~RelieveAfter() {
+        if (on) relieve_retired();
+    }
+};
+
+// *grew: a slot's buffer was replaced (the old one retired): the caller runs
+// relieve_retired() once ctx->pipe.mu is released (RelieveAfter)
+int ensure_slots(rsgpu_ctx *ctx, size_t bytes, bool *grew) {
     auto &P = ctx->pipe;
     while ((int)P.slots.size() < pipe_slots()) {
         std::unique_ptr<PipeSlot> s(new PipeSlot());
@@ -113,7 +126,7 @@ int ensure_slots(rsgpu_ctx *ctx, size_t bytes) {
         s->cap = 0;
         HIP_TRY(hipMalloc(&s->d, cap));
         s->cap = cap;
-        relieve_retired();  // the kept bytes stay bounded (devmem.cpp)
+        *grew = true;  // the kept bytes stay bounded: relieve_retired, after the lock (devmem.cpp)
     }
     return RSGPU_OK;
 }
@@ -163,9 +176,14 @@ void pin_add(void *p, size_t len, size_t readable) {
     std::lock_guard<std::mutex> g(g_pin_mu);
     g_pinned[(uintptr_t)p] = {len, readable, (uintptr_t)d};
 }
-void pin_del(const void *p) {
+// removes p's range; returns its readable length (0: p was not pinned here)
+size_t pin_del(const void *p) {
     std::lock_guard<std::mutex> g(g_pin_mu);
-    g_pinned.erase((uintptr_t)p);
+    auto it = g_pinned.find((uintptr_t)p);
+    if (it == g_pinned.end()) return 0;
+    const size_t readable = it->second.readable;
+    g_pinned.erase(it);
+    return readable;
 }
 
 }  // namespace
@@ -239,8 +257,11 @@ int rsgpu_set_slab_bytes(size_t bytes) {
 
 int rsgpu_host_free(void *p) {
     if (!p) return RSGPU_OK;
-    pin_del(p);
-    return free_user(p, true);
+    // the allocation's size from the pin table (the runtime's address-range
+    // queries do not know every hipHostMalloc'd pointer): the kept-bytes bound
+    // counts a held-back user free by it
+    const size_t bytes = pin_del(p);
+    return free_user(p, true, bytes);
 }
 
 }  // extern "C"
@@ -314,8 +335,9 @@ int rsgpu_encode_batch(rsgpu_ctx *ctx, uint8_t *const *objs, const size_t *shard
     auto img = [&](int o) { return (size_t)n * shard_lens[o]; };
     auto base = [&](int o) { return (const uint8_t *)objs[o]; };
     const std::vector<Group> groups = make_groups(piped, img, base, &maxbytes);
+    RelieveAfter relieve;  // destroyed after g: runs with pipe.mu released
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
-    if ((e = ensure_slots(ctx, maxbytes))) return e;
+    if ((e = ensure_slots(ctx, maxbytes, &relieve.on))) return e;
     hipError_t he = hipSuccess;
     for (size_t gi = 0; gi < groups.size() && he == hipSuccess; ++gi) {
         size_t q = groups[gi].begin;
@@ -418,8 +440,9 @@ int rsgpu_decode_batch(rsgpu_ctx *ctx, uint8_t *const *shards, const uint8_t *pr
     };
     auto base = [&](int o) { return (const uint8_t *)shards[(size_t)o * n]; };
     const std::vector<Group> groups = make_groups(piped, img, base, &maxbytes);
+    RelieveAfter relieve;  // destroyed after g: runs with pipe.mu released
     std::lock_guard<std::mutex> g(ctx->pipe.mu);
-    if ((e = ensure_slots(ctx, maxbytes))) return e;
+    if ((e = ensure_slots(ctx, maxbytes, &relieve.on))) return e;
     if ((e = ensure_flags(ctx, nobj))) return e;
     hipError_t he = hipSuccess;
     for (size_t gi = 0; gi < groups.size() && he == hipSuccess; ++gi) {

@@ -135,9 +135,11 @@ int check_shards(const size_t *lens, int n, bool nilok, size_t *size) {
 
 namespace {
 
+#ifdef RSGPU_MEASURE_DMA_SPLIT
 // The copy-engine share of a split per-object call, percent of the columns
 // (run_host_once; RSGPU_DMA_SPLIT, read once; 0 = off), for objects whose
-// shards are at least kDmaSplitMin bytes
+// shards are at least kDmaSplitMin bytes.  A measurement build only
+// (make HIPFLAGS+=-DRSGPU_MEASURE_DMA_SPLIT): measured 4x slower and not kept.
 constexpr size_t kDmaSplitMin = (size_t)64 << 10;
 int dma_split_pct() {
     static const int v = [] {
@@ -147,6 +149,7 @@ int dma_split_pct() {
     }();
     return v;
 }
+#endif
 
 // Runs `plan` over one object staged from host buffers.  in_src[c] is the
 // host source of staging row plan.in_rows[c]; out_dst[r] receives written
@@ -196,7 +199,7 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         return j;
     };
     hipError_t he = hipSuccess;
-    bool staged_in = false;  // the inputs were copied into the slot's pinned image s->h
+    [[maybe_unused]] bool staged_in = false;  // the inputs were copied into the slot's pinned image s->h (the DMA-split measurement reads it)
     const uint8_t *span0 = in_src[0] - (size_t)(plan.in_rows[0] - rlo) * size;
     bool split = pin_in;
     for (int c = 0; c < plan.K && split; ++c)
@@ -276,8 +279,10 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         L.out_base = s->hdev;
         L.out_dual = then != nullptr;
     }
+#ifdef RSGPU_MEASURE_DMA_SPLIT
+    bool two = false;
     // Copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent>; a
-    // measurement, off by default): the input rows' last columns [cb, size)
+    // measurement build only, not in the product library): the input rows' last columns [cb, size)
     // go H2D on a second stream and a second pass codes them from HBM while
     // the first pass codes columns [0, cb) over PCIe.  Measured 4x slower at
     // 1 MiB — each row slice's copy command carries a fixed ~10-14 us — and
@@ -286,7 +291,6 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
     // share's last vector may reach into the second's first vector, where
     // both passes store the same bytes (the coding of the same input
     // columns).  Both passes set the same mapped check flag.
-    bool two = false;
     if (he == hipSuccess && L.in_base && size >= kDmaSplitMin && dma_split_pct() > 0) {
         const size_t blen = (size * (size_t)dma_split_pct() / 100) & ~(size_t)15;
         if (blen >= 4096 && blen + 16 <= size) {
@@ -315,13 +319,16 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
             }
         }
     }
+#endif
     if (he == hipSuccess) he = launch_plan(plan, L, s->m_bad, s->stream);
     // what follows on the slot's stream (D2H of written rows, the `then`
     // pass over the image) waits for the second share
+#ifdef RSGPU_MEASURE_DMA_SPLIT
     if (two && he == hipSuccess && (!L.out_base || then)) {
         he = hipEventRecord(s->ev2, s->stream2);
         if (he == hipSuccess) he = hipStreamWaitEvent(s->stream, s->ev2, 0);
     }
+#endif
     auto dst = [&](size_t r) {
         return pin_out ? (const uint8_t *)out_dst[r] : (const uint8_t *)s->h + (size_t)orows[r] * size;
     };
@@ -341,11 +348,15 @@ int run_host_once(rsgpu_ctx *ctx, Plan &plan, int nrows_staged, size_t size,
         img.slack = true;
         he = launch_plan(*then, img, s->m_bad, s->stream);
     }
+#ifdef RSGPU_MEASURE_DMA_SPLIT
     if (he == hipSuccess && two) he = hipStreamSynchronize(s->stream2);
+#endif
     if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
     if (he != hipSuccess) {
         (void)hipStreamSynchronize(s->stream);  // nothing in flight may touch a pooled slot
+#ifdef RSGPU_MEASURE_DMA_SPLIT
         if (s->stream2) (void)hipStreamSynchronize(s->stream2);
+#endif
         ctx->put_slot(std::move(s));
         return hip_fail(he, "run_host");
     }

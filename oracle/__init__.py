@@ -73,6 +73,9 @@ def lib():
         L.orc_code_batch.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ip, ip, u8p, ctypes.c_size_t,
                                      ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
         L.orc_code_batch.restype = None
+        L.orc_verify_batch.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ip, ip, u8p, ctypes.c_size_t,
+                                       ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ip]
+        L.orc_verify_batch.restype = None
         _lib = L
     return _lib
 
@@ -169,3 +172,18 @@ def code_batch(coef, in_rows, out_rows, base: np.ndarray, obj_stride, pitch, len
     orr = (ctypes.c_int * len(out_rows))(*out_rows)
     lib().orc_code_batch(_u8p(coef), coef.shape[0], coef.shape[1], ir, orr, _u8p(base),
                          obj_stride, pitch, length, nobj, nthreads)
+
+
+def verify_batch(coef, in_rows, chk_rows, base: np.ndarray, obj_stride, pitch, length, nobj,
+                 nthreads=1):
+    """Batch Verify over a [obj][shard][pitch] host buffer: per object, rows
+    coef x in_rows recomputed and compared with the stored rows chk_rows
+    (upstream Verify when coef = the parity rows over the data rows).
+    Returns the per-object ok flags (uint8 array)."""
+    coef = np.ascontiguousarray(coef, dtype=np.uint8)
+    ir = (ctypes.c_int * len(in_rows))(*in_rows)
+    cr = (ctypes.c_int * len(chk_rows))(*chk_rows)
+    ok = (ctypes.c_int * max(1, nobj))()
+    lib().orc_verify_batch(_u8p(coef), coef.shape[0], coef.shape[1], ir, cr, _u8p(base),
+                           obj_stride, pitch, length, nobj, nthreads, ok)
+    return np.array(ok[:nobj], dtype=np.uint8)

@@ -570,3 +570,44 @@ void orc_code_batch(const uint8_t *coef, int nrows, int ninputs, const int *in_r
     bjob_t j = {coef, nrows, ninputs, in_rows, out_rows, base, obj_stride, pitch, len};
     pool_run(obj_task, &j, nobj, nthreads);
 }
+
+/* Batch Verify (upstream Verify / checkSomeShards): object o's rows
+ * coef x inputs are recomputed block by block into a task-local buffer and
+ * compared with its stored rows chk_rows (the parity upstream's Verify
+ * re-encodes, or the fused Get's extra parity shards); ok[o] = 1 when every
+ * stored row matches.  Object-parallel like orc_code_batch. */
+typedef struct {
+    const uint8_t *coef; int nrows, ninputs;
+    const int *in_rows, *chk_rows;
+    const uint8_t *base; size_t obj_stride, pitch, len;
+    int *ok;
+} vjob_t;
+
+#define ORC_VBLOCK ((size_t)64 << 10)
+static void verify_task(void *arg, int o) {
+    vjob_t *j = (vjob_t *)arg;
+    const uint8_t *rows[256], *ins[256];
+    uint8_t *outs[256];
+    uint8_t *tmp = (uint8_t *)aligned_alloc(64, ORC_VBLOCK * (size_t)j->nrows);
+    for (int r = 0; r < j->nrows; r++) rows[r] = j->coef + (size_t)r * j->ninputs;
+    const uint8_t *ob = j->base + (size_t)o * j->obj_stride;
+    int good = 1;
+    for (size_t s = 0; s < j->len && good; s += ORC_VBLOCK) {
+        const size_t n = j->len - s < ORC_VBLOCK ? j->len - s : ORC_VBLOCK;
+        for (int c = 0; c < j->ninputs; c++) ins[c] = ob + (size_t)j->in_rows[c] * j->pitch + s;
+        for (int r = 0; r < j->nrows; r++) outs[r] = tmp + (size_t)r * ORC_VBLOCK;
+        code_range_fast(rows, j->nrows, ins, j->ninputs, outs, 0, n);
+        for (int r = 0; r < j->nrows && good; r++)
+            if (memcmp(outs[r], ob + (size_t)j->chk_rows[r] * j->pitch + s, n)) good = 0;
+    }
+    free(tmp);
+    j->ok[o] = good;
+}
+
+void orc_verify_batch(const uint8_t *coef, int nrows, int ninputs, const int *in_rows,
+                      const int *chk_rows, const uint8_t *base, size_t obj_stride, size_t pitch,
+                      size_t len, int nobj, int nthreads, int *ok) {
+    gf_init();
+    vjob_t j = {coef, nrows, ninputs, in_rows, chk_rows, base, obj_stride, pitch, len, ok};
+    pool_run(verify_task, &j, nobj, nthreads);
+}

@@ -1,0 +1,68 @@
+"""bench.py's CPU-baseline leg for the checked Get of BASELINE config 3
+(dec4_get / dec4_upstream), no GPU: the oracle's batch Verify
+(oracle.verify_batch, upstream Verify / checkSomeShards) and the CPU decode
+forms bench.py times beside the GPU line.
+
+  * verify_batch flags exactly the objects whose stored rows differ from the
+    recomputed ones (upstream Verify: every parity row re-encoded from the
+    data rows; the fused Get: the extra shards from the survivors);
+  * cpu_baseline on a small RS(10+4) batch with 12 of 14 shards present
+    rebuilds data {0,5} bit-exact and reports both forms (Reconstruct+Verify,
+    client/ecRedis.go:414-420, and the fused one)."""
+import numpy as np
+
+import bench
+import oracle
+from oracle import rs_numpy as rn
+
+
+def _batch(k, p, nobj, S, pitch, seed):
+    n = k + p
+    rng = np.random.default_rng(seed)
+    b = np.zeros((nobj, n, pitch), dtype=np.uint8)
+    b[:, :k, :S] = rng.integers(0, 256, (nobj, k, S), dtype=np.uint8)
+    m = rn.build_matrix(k, p)
+    oracle.code_batch(m[k:], list(range(k)), list(range(k, n)), b.reshape(-1), n * pitch, pitch, S, nobj)
+    return b, m
+
+
+def test_verify_batch_flags_exactly_the_corrupt_objects():
+    k, p, nobj, S, pitch = 10, 4, 7, 1000, 1024
+    n = k + p
+    b, m = _batch(k, p, nobj, S, pitch, 1)
+    ok = oracle.verify_batch(m[k:], list(range(k)), list(range(k, n)), b.reshape(-1), n * pitch, pitch, S,
+                             nobj, nthreads=4)
+    assert ok.tolist() == [1] * nobj
+    b[3, 13, S - 1] ^= 1   # parity row, last byte
+    b[5, 2, 0] ^= 0x80     # a data row: every parity row disagrees
+    ok = oracle.verify_batch(m[k:], list(range(k)), list(range(k, n)), b.reshape(-1), n * pitch, pitch, S,
+                             nobj, nthreads=4)
+    assert ok.tolist() == [1, 1, 1, 0, 1, 0, 1]
+    # the fused Get's checks: extra shards 12, 13 from the survivors
+    surv = [1, 2, 3, 4, 6, 7, 8, 9, 10, 11]
+    b, m = _batch(k, p, nobj, S, pitch, 2)
+    coef = rn.matmul(m[[12, 13]], rn.invert(m[surv]))
+    b[6, 12, 500] ^= 0x11
+    ok = oracle.verify_batch(coef, surv, [12, 13], b.reshape(-1), n * pitch, pitch, S, nobj, nthreads=2)
+    assert ok.tolist() == [1] * 6 + [0]
+
+
+def test_cpu_baseline_checked_get_forms():
+    w = dict(bench.WORKLOADS["dec4_get"])
+    w["nbytes"] = 40 << 10
+    k, p = w["k"], w["p"]
+    n = k + p
+    S = (w["nbytes"] + k - 1) // k
+    pitch = (S + 255) // 256 * 256
+    gpu_sample, m = _batch(k, p, 6, S, pitch, 3)
+    sample = gpu_sample.copy()
+    sample[:, list(w["lost"])] = 0
+    surv = [i for i in range(n) if i not in w["lost"]][:k]
+    inv_rows = rn.invert(m[surv])[list(w["lost"])]
+    cpu = bench.cpu_baseline(w, sample, gpu_sample, m, inv_rows, budget_s=0.5, threads=2, windows=1,
+                             fused_checks=2)
+    assert cpu["kind"] == "port" and cpu["value"] > 0
+    assert cpu["fused_form_GiBps"] > 0
+    assert "Reconstruct then Verify" in cpu["decode_form"]
+    assert "bit-exact vs GPU (parity, and the rows the GPU rebuilt from garbage in the work check): True" \
+        in cpu["sample"]

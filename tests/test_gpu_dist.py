@@ -152,6 +152,32 @@ def test_bench_two_ranks_shared_gpu(gpu, tmp_path):
     assert st["value"] > 0 and st["ms_per_step"] > 0
 
 
+def test_bench_four_ranks_shared_gpu_uneven(gpu):
+    """N = 4 of bench.py's multi-rank path on the one-GPU box (gloo, ranks
+    sharing cuda:0), with a batch that does not divide evenly: the strong
+    block splits 50 objects 13 + 13 + 12 + 12 (shard_objects), every object
+    coded once; each rank's weak batch is checked bit-exact; the per-rank
+    roofline has 4 entries."""
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo", BENCH_SHARE_GPU="1", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "3", "--warmup", "2",
+           "--batch", "50", "--cpu-seconds", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["config"]["batch_per_gpu"] == 50
+    assert all(v["result"] == "bit-exact" for v in out["work_check"].values())
+    assert len(out["roofline"]["frac_per_rank"]) == 4 and min(out["roofline"]["frac_per_rank"]) > 0
+    st = out["strong_scaling"]
+    assert st["batch_total"] == 50 and st["objects_coded"] == 50
+    assert st["objects_per_rank"] == [13, 13, 12, 12]
+    assert out["work_check_ranks"] == [1, 1, 1, 1]
+    assert out["cpu_baseline"] is not None and out["cpu_baseline"]["sample"].endswith(": True")
+
+
 def test_bench_one_rank_rccl(gpu):
     """BASELINE config 4's collectives on the one-GPU box: bench.py under
     torch.distributed.run with ONE rank, the default nccl (RCCL) backend and

@@ -418,6 +418,64 @@ def test_dev_rs10_4_4mib_decode_all_2data_patterns(gpu):
             assert np.array_equal(h[o, k + r, :S], want[r])
 
 
+def test_dev_rs10_4_4mib_get_with_checks_batch512(gpu):
+    """BASELINE config 3 as Client.decode runs it (client/ecRedis.go:404-427),
+    at bench.py dec4_get's full size: 512 x 4 MiB objects, 12 of 14 shards
+    present, data {0,5} rebuilt from the first 10 present and the 2 extra
+    parity shards checked in the same pass.  Rebuilt rows are bit-exact with
+    the oracle's restatement over the whole batch; one corrupted byte in an
+    extra parity row flags exactly its object (first byte of row 12 in one
+    object, last byte of row 13 in another), and the unfused upstream form
+    (Reconstruct, then Verify) flags the same two."""
+    k, p, S, nobj = 10, 4, 419431, 512
+    n = k + p
+    pitch = (S + 255) // 256 * 256
+    stride = n * pitch
+    lost = (0, 5)
+    present = [i not in lost for i in range(n)]
+    surv = [i for i in range(n) if present[i]][:k]
+    enc = ia.New(k, p)
+    s = torch.cuda.current_stream()
+    b = _dev_batch(nobj, n, S, pitch, seed=101)
+    enc.encode_dev(b, S, pitch, stride, nobj, s)
+    torch.cuda.synchronize()
+    h = b.cpu().numpy()
+    m = enc.matrix()
+    ref = h.copy()
+    ref[:, k:] = 0
+    oracle.code_batch(m[k:], list(range(k)), list(range(k, n)), ref.reshape(-1), stride, pitch, S, nobj,
+                      nthreads=16)
+    assert np.array_equal(h[:, :, :S], ref[:, :, :S])  # parity of the whole batch vs the oracle
+    # the oracle's Reconstruct of {0,5} from the same first 10 present rows
+    ref[:, k:] = h[:, k:]
+    ref[:, list(lost)] = 0
+    e, inv = oracle.invert(m[surv])
+    assert e == 0
+    inv_rows = inv[list(lost)]
+    oracle.code_batch(inv_rows, surv, list(lost), ref.reshape(-1), stride, pitch, S, nobj, nthreads=16)
+    del h
+    bad_objs = (200, 311)
+    b[200, 12, 0] ^= 0x01
+    b[311, 13, S - 1] ^= 0x5A
+    b[:, 0].fill_(0xA5)
+    b[:, 5].fill_(0x3C)
+    bad = torch.full((nobj,), 7, dtype=torch.int32, device="cuda")
+    enc.decode_dev(b, present, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert torch.nonzero(bad).flatten().tolist() == list(bad_objs)
+    got = b[:, list(lost), :S].cpu().numpy()
+    assert np.array_equal(got, ref[:, list(lost), :S])
+    # upstream's two passes on the same batch: same rows, same two flags
+    b[:, 0].fill_(0)
+    b[:, 5].fill_(0)
+    bad.fill_(7)
+    enc.reconstruct_dev(b, present, S, pitch, stride, nobj, data_only=False, stream=s)
+    enc.verify_dev(b, S, pitch, stride, nobj, bad, s)
+    torch.cuda.synchronize()
+    assert torch.nonzero(bad).flatten().tolist() == list(bad_objs)
+    assert np.array_equal(b[:, list(lost), :S].cpu().numpy(), ref[:, list(lost), :S])
+
+
 def test_dev_verify_flags_per_object(gpu):
     k, p, S, nobj = 10, 2, 5001, 9
     pitch = 5120

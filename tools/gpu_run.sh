@@ -71,7 +71,7 @@ PY
             done ;;
     trace_alloc) run trace_coherent 900 python bench.py --workload trace --steps 3 --warmup 1
             RSGPU_HOST_ALLOC=default run trace_default 900 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu ;;
-    dma_split) # the copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent of columns>), 1 MiB per object
+    dma_split) # the copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent of columns>), 1 MiB per object; needs a measurement build: make -C infinicache_amd/csrc HIPFLAGS+=-DRSGPU_MEASURE_DMA_SPLIT
             RSGPU_DMA_SPLIT=40 run pytest_dma_split 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random.py tests/test_c_abi.py -m gpu -x -q --timeout 150 --timeout-method thread
             for rep in 1 2; do
               for pct in ${DMA_PCTS:-0 20 30 40 50}; do
@@ -108,6 +108,17 @@ PY
     rccl1)  # BASELINE config 4's collectives over RCCL with one rank (the -m gpu test writes the line)
             BENCH_RCCL_JSON=gpurun_out/r05_bench_rccl_1rank.json run pytest_rccl1 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -x -v -s --timeout 240 --timeout-method thread ;;
     avail)  run avail 120 rocprofv3 --list-avail ;;
+    dec4get) # BASELINE config 3 as Client.decode runs it: fused and unfused Get lines + kernel stats
+            for wl in dec4_get dec4_upstream; do
+              run bench_$wl 600 python bench.py --workload $wl
+              run prof_$wl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$wl -o run --output-format csv -- python3 bench.py --no-cpu --no-pmc --steps 20 --workload $wl
+            done ;;
+    sq)     # issue / wait / clock counters per kernel (one pass per workload; 8 SQ + 2 GRBM slots)
+            for wl in ${SQ_WLS:-dec4_get encdec}; do
+              run sq_$wl 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/sq_$wl -o run --output-format csv -- python3 bench.py --no-cpu --no-pmc --steps 5 --warmup 50 --workload $wl
+            done ;;
+    rehearse8) # the N = 8 scaling harness on the one-GPU box (8 gloo ranks sharing cuda:0), full batch
+            BENCH_DIST_BACKEND=gloo BENCH_SHARE_GPU=1 run rehearse8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 ;;
     pcie)   run pcie 300 ./tools/pcie_bench ;;
     example) run example 300 python examples/client_example.py --loopback --addr 127.0.0.1:16378 ;;
     rehearse2) BENCH_DIST_BACKEND=gloo BENCH_SHARE_GPU=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --no-cpu --copies 2 ;;
