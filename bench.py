@@ -167,6 +167,17 @@ METRICS = {
 }
 
 
+def pass_symbol(K, R, KI, S, shard_major=False):
+    """Kernel a uniform K-input, R-row pass of the library runs (KI trailing
+    identity inputs, shard length S): gf_apply_tri for the shapes
+    infinicache_amd/csrc/gf_kernels.hip tri_shape lists, on rows longer than
+    128 16-B vectors of an object-major batch; gf_apply_kernel otherwise."""
+    tri = {(12, 4, 2), (11, 4, 1), (10, 4, 0), (14, 4, 4), (13, 3, 3), (16, 4, 4)}
+    if (K, R, KI) in tri and (S + 15) // 16 * 2 > 256 and not shard_major:
+        return f"gf_apply_tri<{K},{R}>"
+    return f"gf_apply_kernel<{K},{R}>"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -1121,8 +1132,9 @@ def main():
     # included (upstream Reconstruct, ecRedis.go:415), unless ReconstructData);
     # upstream's separate Verify reads all k+p rows
     dec_in = k + fused_checks
-    enc_sym = f"gf_apply_kernel<{k},{p}>"
-    dec_sym = f"gf_apply_kernel<{dec_in},{e_rows + fused_checks}>"
+    sm = bool(w.get("shard_major"))
+    enc_sym = pass_symbol(k, p, 0, S, sm)
+    dec_sym = pass_symbol(dec_in, e_rows + fused_checks, fused_checks, S, sm)
     if k > 16:  # generic kernel, one launch per <= 8 rows
         enc_sym, dec_sym = f"gf_apply_generic<{min(p, 8)}>", f"gf_apply_generic<{e_rows}>"
     if w.get("mixed"):  # device-resolved patterns: KMAX = n inputs (gf_masked.h)
@@ -1131,8 +1143,8 @@ def main():
     unit_info = {
         "encode": (enc_sym, nobj * n * S, nobj * k * S),
         "decode": (dec_sym, nobj * (dec_in + e_rows) * S, nobj * dec_in * S),
-        "decode:reconstruct": (f"gf_apply_kernel<{k},{e_rows}>", nobj * (k + e_rows) * S, nobj * k * S),
-        "decode:verify": (f"gf_apply_kernel<{n},{p}>", nobj * n * S, nobj * n * S),
+        "decode:reconstruct": (pass_symbol(k, e_rows, 0, S, sm), nobj * (k + e_rows) * S, nobj * k * S),
+        "decode:verify": (pass_symbol(n, p, p, S, sm), nobj * n * S, nobj * n * S),
     }
     # launches grouped by kernel symbol: encode and the uniform-pattern decode
     # of RS(10+2) are the same kernel (gf_apply_kernel<10,2>) with the same

@@ -146,6 +146,10 @@ hipError_t launch_plan_objs(Plan &p, const DevObj *objs, int nobj, uint32_t *d_b
 // zeroed by the caller when the plan has check rows.  Returns hipSuccess or
 // the first HIP error.
 hipError_t launch_plan(Plan &plan, const Layout &L, uint32_t *d_bad, hipStream_t stream);
+// Whether the passes of gf_apply_tri's shapes take it (gf_kernels.hip): 1
+// (default) or 0 (the single-input kernel).  Measurement (tools/kbench);
+// RSGPU_TRI sets it at load.
+void set_tri_mode(int mode);
 
 // Device atlas of every erasure pattern of one operation (gf_masked.h): the
 // pattern table over all 2^n present masks, one record per (pattern,

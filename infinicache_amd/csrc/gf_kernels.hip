@@ -300,6 +300,185 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
 
 inline unsigned generic_lds(int K, int R) { return (unsigned)((K * R + 1) / 2 * 16 + K / 3 * R * 32); }
 
+// Specialised passes (K <= 16) that are VALU-bound and store rows: the
+// generic kernel's input triples, with K, R and the trailing identity inputs
+// KI known at compile time.  The fused Get of RS(10+4) with 2 extra parity
+// shards (K = 12, R = 4: 2 rows written, 2 checked, KI = 2) issued 1,197
+// VALU instructions per wave with single inputs, at 84 % VALUBusy and a
+// 2.24 GHz held clock against the headline encode's 52 % and 2.40 GHz
+// (profiles/r06_sq_dec4_get.json): the SIMDs' issue, not HBM, set its time.
+//   * the G = K - KI GF inputs go as NT = G / 3 triples (8 v_perm + 4 xor3
+//     per row and dword for three inputs), the G mod 3 rest as one input or a
+//     pair through the 5-word tables; identity inputs are one XOR each;
+//   * the low halves of the triple tables are SGPRs (s_load from the plan's
+//     device image), the high halves and the single inputs' words 1 and 3 are
+//     staged in LDS once per workgroup (GFX9's constant bus: one SGPR per
+//     lookup), so no lookup waits for a v_mov;
+//   * every input row is loaded up front (K loads in flight per lane, as the
+//     single-input kernel); VW = 4 (16-B lanes; 8-B lanes measured slower).
+// Tables: the generic kernel's device image (upload_generic: [K][R] single
+// words, [K/3][R][16] triples over inputs [0, 3 NT), which are the first
+// NT triples of the GF inputs).
+template <int K>
+struct TriArgs {
+    const uint8_t *base;
+    uint64_t obj_stride;
+    uint32_t *bad;
+    const uint32_t *tab;   // [K][rstride][kTabWords]
+    const uint32_t *tab3;  // [K/3][rstride][16]
+    uint32_t nvec, tail, nw, span, rstride, clear, packed;
+    Order ord;  // item = object
+    uint32_t in_off[K];
+    uint32_t out_off[kMaxR];
+};
+
+template <int K, int R, int KI>
+struct TriShape {
+    static constexpr int G = K - KI, NT = G / 3, NS = G - 3 * NT;
+    // LDS: [NS][R] u32x2 words 1 and 3 of the rest inputs, then [NT][R][2]
+    // u32x4 high halves of the triple tables
+    static constexpr unsigned lds = (unsigned)((NS * R + 1) / 2 * 16 + NT * R * 32);
+};
+
+template <int K, int R, int KI, int VW>
+__global__ __launch_bounds__(kBlock) void gf_apply_tri(const TriArgs<K> a) {
+    using Sh = TriShape<K, R, KI>;
+    constexpr int G = Sh::G, NT = Sh::NT, NS = Sh::NS;
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    extern __shared__ u32x4 lds_tab[];
+    u32x2 *lvw = (u32x2 *)lds_tab;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(NS * R); i += kBlock) {
+        const uint32_t c = 3 * NT + i / R, r = i % R;
+        const uint32_t *e = a.tab + ((size_t)c * a.rstride + r) * kTabWords;
+        lvw[i] = u32x2{e[1], e[3]};
+    }
+    u32x4 *lv3 = lds_tab + (NS * R + 1) / 2;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(NT * R * 2); i += kBlock) {
+        const uint32_t tr = i >> 1, t = tr / R, r = tr - t * R;
+        const uint32_t *e = a.tab3 + ((size_t)t * a.rstride + r) * 16 + 8 + (i & 1) * 4;
+        lv3[i] = u32x4{e[0], e[1], e[2], e[3]};
+    }
+    __syncthreads();
+    const uint32_t v = chunk * kBlock + threadIdx.x;
+    if (v >= a.nvec) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)obj * a.obj_stride), (short)0, (int)a.span, 0x00020000);
+    const uint32_t voff = v * (4u * VW);
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        if (VW == 4) {
+            x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, a.in_off[c], kLoadAux);
+        } else {
+            const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, a.in_off[c], kLoadAux);
+            x[c] = u32x4{t[0], t[1], 0u, 0u};
+        }
+    }
+    uint32_t acc[R][VW];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int d = 0; d < VW; ++d) acc[r][d] = 0;
+    // one triple (or rest group) at a time: without the fences the scheduler
+    // hoists every group's selector math and the registers run out
+    auto fence = [&] {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int d = 0; d < VW; ++d) asm volatile("" : "+v"(acc[r][d]));
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    const constant_ptr<uint32_t> tab = (constant_ptr<uint32_t>)a.tab;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const u32x4 &xa = x[3 * t], &xb = x[3 * t + 1], &xc = x[3 * t + 2];
+        uint32_t sel[VW][8];
+#pragma unroll
+        for (int d = 0; d < VW; ++d) {
+            sel[d][0] = xa[d] & 0x07070707u;
+            sel[d][1] = (xa[d] >> 3) & 0x07070707u;
+            sel[d][2] = xb[d] & 0x07070707u;
+            sel[d][3] = (xb[d] >> 3) & 0x07070707u;
+            sel[d][4] = xc[d] & 0x07070707u;
+            sel[d][5] = (xc[d] >> 3) & 0x07070707u;
+            sel[d][6] = ((xa[d] >> 5) & 0x06060606u) | ((xb[d] >> 7) & 0x01010101u);
+            sel[d][7] = ((xb[d] >> 6) & 0x01010101u) | ((xc[d] >> 5) & 0x06060606u);
+        }
+        const constant_ptr<uint32_t> T = (constant_ptr<uint32_t>)a.tab3 + (size_t)t * a.rstride * 16;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const constant_ptr<uint32_t> L = T + r * 16;
+            const u32x4 h0 = lv3[(t * R + r) * 2], h1 = lv3[(t * R + r) * 2 + 1];
+#pragma unroll
+            for (int d = 0; d < VW; ++d) {
+                uint32_t q = xor3(acc[r][d], lut8(L[0], h0[0], sel[d][0]), lut8(L[1], h0[1], sel[d][1]));
+                q = xor3(q, lut8(L[2], h0[2], sel[d][2]), lut8(L[3], h0[3], sel[d][3]));
+                q = xor3(q, lut8(L[4], h1[0], sel[d][4]), lut8(L[5], h1[1], sel[d][5]));
+                acc[r][d] = xor3(q, lut8(L[6], h1[2], sel[d][6]), lut8(L[7], h1[3], sel[d][7]));
+            }
+        }
+        fence();
+    }
+    if constexpr (NS == 2) {  // a pair: 6 lookups and 3 xor3 per row and dword
+        constexpr int c = 3 * NT;
+        const constant_ptr<uint32_t> ta = tab + (size_t)c * a.rstride * kTabWords;
+        const constant_ptr<uint32_t> tb = ta + (size_t)a.rstride * kTabWords;
+#pragma unroll
+        for (int d = 0; d < VW; ++d) {
+            const GfIdx ga = gf_idx(x[c][d]), gb = gf_idx(x[c + 1][d]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const constant_ptr<uint32_t> A = ta + r * kTabWords, B = tb + r * kTabWords;
+                const u32x2 wa = lvw[r], wb = lvw[R + r];
+                uint32_t s = xor3(acc[r][d], lut8(A[0], wa[0], ga.i0), lut8(A[2], wa[1], ga.i1));
+                s = xor3(s, lut8(A[4], A[4], ga.i2), lut8(B[0], wb[0], gb.i0));
+                acc[r][d] = xor3(s, lut8(B[2], wb[1], gb.i1), lut8(B[4], B[4], gb.i2));
+            }
+        }
+        fence();
+    } else if constexpr (NS == 1) {
+        constexpr int c = 3 * NT;
+        const constant_ptr<uint32_t> ta = tab + (size_t)c * a.rstride * kTabWords;
+#pragma unroll
+        for (int d = 0; d < VW; ++d) {
+            const GfIdx g = gf_idx(x[c][d]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const constant_ptr<uint32_t> A = ta + r * kTabWords;
+                const u32x2 w = lvw[r];
+                const uint32_t s = xor3(acc[r][d], lut8(A[0], w[0], g.i0), lut8(A[2], w[1], g.i1));
+                acc[r][d] = s ^ lut8(A[4], A[4], g.i2);
+            }
+        }
+        fence();
+    }
+    // identity inputs: input G + j feeds row R - KI + j with coefficient 1
+#pragma unroll
+    for (int j = 0; j < KI; ++j)
+#pragma unroll
+        for (int d = 0; d < VW; ++d) acc[R - KI + j][d] ^= x[G + j][d];
+    bool mismatch = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if ((uint32_t)r < a.nw) {
+            if (VW == 4) {
+                const u32x4 o = {acc[r][0], acc[r][1], acc[r][VW > 2 ? 2 : 0], acc[r][VW > 3 ? 3 : 0]};
+                store_row<kStoreAux>(o, rs, voff, a.out_off[r], v == a.nvec - 1 ? a.packed : 0u);
+            } else {
+                store_row8<kStoreAux>(u32x2{acc[r][0], acc[r][1]}, rs, voff, a.out_off[r],
+                                      v == a.nvec - 1 ? a.packed : 0u);
+            }
+        } else {
+            const uint32_t valid = (v == a.nvec - 1) ? a.tail : 4u * VW;
+#pragma unroll
+            for (int d = 0; d < VW; ++d) mismatch |= (acc[r][d] & tail_mask(d, valid)) != 0;
+        }
+    }
+    if (mismatch) a.bad[obj] = 1u;  // same value from every writer: no atomic needed
+    if (a.clear && v == 0) a.bad[obj] = 0u;
+}
+
 // ----------------------------------------------------------------- launchers
 
 namespace {
@@ -421,10 +600,17 @@ hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *
 template <int K, int R>
 hipError_t launch_fixed3(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad, hipStream_t st);
 
+// the triples kernel for this pass, when it has one (launch_tri, below);
+// returns false when the pass takes the single-input kernel
+template <int K, int R>
+bool launch_tri(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad, hipStream_t st, hipError_t &e);
+
 template <int K, int R>
 hipError_t launch_fixed(const Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad,
                         hipStream_t st) {
     if constexpr (R >= 3 && K >= 6) {
+        hipError_t e = hipSuccess;
+        if (launch_tri<K, R>(p, s, L, d_bad, st, e)) return e;
         const int ki = (s.r0 + R == p.R) ? std::min(p.ki, R) : 0;
         if (!L.in_base && !L.out_base && use_triples(K, R, ki, s.nw)) return launch_fixed3<K, R>(p, s, L, d_bad, st);
     }
@@ -822,6 +1008,108 @@ hipError_t launch_generic(Plan &p, const Sub &s, const Layout &L, uint32_t *d_ba
     return hipSuccess;
 }
 
+// Which passes take gf_apply_tri (set_tri_mode): 1 (default) every pass of
+// an instantiated shape (tri_shape) over rows longer than 128 vectors; 0 none
+// (the single-input kernel and, for check-only passes, its Pass3 triples).
+// Cold, tools/kbench KB_SET=tri (profiles/r06_kbench_tri_*.txt), single
+// inputs -> gf_apply_tri:
+//   fused Get RS(10+4), 2 extra shards, 4 MiB: 72.7 -> 72.5 % (HBM-bound at
+//     that size: VALUBusy 84 -> 68 %, WAIT_ANY 31 -> 55 % of wave cycles);
+//     1 MiB 70.5 -> 72.6 %
+//   encode RS(10+4) 4 MiB 73.5 -> 74.3 %;  Verify RS(10+4) 82.7 -> 87.9 %
+//   (the XOR-only kernel on the same streams: 88.3 %)
+// 8-B lanes lost 1.6-6.5 points on every shape (66.0 / 67.3 / 69.7 / 84.5 %).
+// RSGPU_TRI sets the mode at load (measurement)
+int env_int(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+std::atomic<int> g_tri_mode{env_int("RSGPU_TRI", 1)};
+
+// (K, R, KI) shapes with a gf_apply_tri instantiation: the fused RS(10+4) Get
+// with 2 extra shards (12, 4, 2) or 1 (11, 4, 1: 3 data shards lost), the
+// RS(10+4) encode (10, 4, 0), and Verify of RS(10+4) (14, 4, 4), RS(10+3)
+// (13, 3, 3) and RS(12+4) (16, 4, 4).  bench.py's kernel names follow this
+// list (bench.py tri_shape).
+constexpr bool tri_shape(int K, int R, int KI) {
+    return (K == 12 && R == 4 && KI == 2) || (K == 11 && R == 4 && KI == 1) || (K == 10 && R == 4 && KI == 0) ||
+           (K == 14 && R == 4 && KI == 4) || (K == 13 && R == 3 && KI == 3) || (K == 16 && R == 4 && KI == 4);
+}
+
+template <int K, int R, int KI, int VW>
+hipError_t launch_tri_k(Plan &p, const Sub &s, const Layout &L, uint32_t *d_bad, hipStream_t st) {
+    using Sh = TriShape<K, R, KI>;
+    constexpr uint32_t vb = 4u * VW;  // bytes per lane vector
+    TriArgs<K> a;
+    a.obj_stride = L.obj_stride;
+    a.nvec = (uint32_t)((L.shard_len + vb - 1) / vb);
+    a.tail = (uint32_t)(L.shard_len - (size_t)(a.nvec - 1) * vb);
+    a.nw = (uint32_t)s.nw;
+    a.rstride = (uint32_t)p.R;
+    a.tab = p.d_tab + (size_t)s.r0 * kTabWords;
+    a.tab3 = p.d_tab3 + (size_t)s.r0 * 16;
+    a.clear = (d_bad && p.nw == p.R) ? 1u : 0u;
+    {
+        const size_t w = row_space(L) - (size_t)(a.nvec - 1) * vb;
+        a.packed = w < vb ? (uint32_t)w : 0u;
+    }
+    int maxrow = 0;
+    for (int c = 0; c < K; ++c) {
+        a.in_off[c] = (uint32_t)(p.in_rows[c] * L.pitch);
+        maxrow = std::max(maxrow, p.in_rows[c]);
+    }
+    for (int r = 0; r < kMaxR; ++r) {
+        const int row = r < R ? p.out_rows[s.r0 + r] : 0;
+        a.out_off[r] = (uint32_t)((row < 0 ? 0 : row) * L.pitch);
+        maxrow = std::max(maxrow, row);
+    }
+    a.span = (uint32_t)((size_t)maxrow * L.pitch + (size_t)a.nvec * vb);
+    const unsigned gx = (a.nvec + kBlock - 1) / kBlock;
+    const int step = max_items(gx);
+    const unsigned lds = std::max(Sh::lds, pass_lds(K, s.nw, R));
+    for (int o0 = 0; o0 < L.nobj; o0 += step) {
+        const int no = std::min(step, L.nobj - o0);
+        a.base = L.base + (size_t)o0 * L.obj_stride;
+        a.bad = d_bad ? d_bad + o0 : nullptr;
+        unsigned grid;
+        a.ord = make_order(gx, (uint32_t)no, objs_span(L, no, a.span), grid);
+        hipLaunchKernelGGL((gf_apply_tri<K, R, KI, VW>), dim3(grid), dim3(kBlock), lds, st, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+template <int K, int R>
+bool launch_tri(const Plan &pc, const Sub &s, const Layout &L, uint32_t *d_bad, hipStream_t st, hipError_t &e) {
+    if (g_tri_mode.load(std::memory_order_relaxed) == 0 || L.in_base || L.out_base || L.sub_stride ||
+        s.r0 != 0 || s.R != pc.R)
+        return false;
+    if ((L.shard_len + 15) / 16 * 2 <= (size_t)kBlock) return false;  // small objects: the packed forms
+    const int ki = std::min(pc.ki, R);
+    Plan &p = const_cast<Plan &>(pc);
+    auto ready = [&]() -> bool {  // the plan's table image (upload_generic), once
+        if (p.dev_done.load(std::memory_order_acquire)) return true;
+        std::lock_guard<std::mutex> g(p.dev_mu);
+        if (!p.dev_done.load(std::memory_order_relaxed)) {
+            if ((e = upload_generic(p)) != hipSuccess) return false;
+            p.dev_done.store(true, std::memory_order_release);
+        }
+        return true;
+    };
+#define RSGPU_TRI(KI_)                                                \
+    if constexpr (tri_shape(K, R, KI_)) {                             \
+        if (ki == KI_) {                                              \
+            if (!ready()) return e != hipSuccess;                     \
+            e = launch_tri_k<K, R, KI_, 4>(p, s, L, d_bad, st);       \
+            return true;                                              \
+        }                                                             \
+    }
+    RSGPU_TRI(0) RSGPU_TRI(1) RSGPU_TRI(2) RSGPU_TRI(3) RSGPU_TRI(4)
+#undef RSGPU_TRI
+    return false;
+}
+
 typedef hipError_t (*fixed_fn)(const Plan &, const Sub &, const Layout &, uint32_t *, hipStream_t);
 
 template <int K>
@@ -916,6 +1204,8 @@ hipError_t launch_huge(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st
 }
 
 }  // namespace
+
+void set_tri_mode(int mode) { g_tri_mode.store(mode, std::memory_order_relaxed); }
 
 hipError_t launch_plan(Plan &p, const Layout &L, uint32_t *d_bad, hipStream_t st) {
     if (L.nobj <= 0 || p.R <= 0) return hipSuccess;

@@ -71,7 +71,7 @@ PY
             done ;;
     trace_alloc) run trace_coherent 900 python bench.py --workload trace --steps 3 --warmup 1
             RSGPU_HOST_ALLOC=default run trace_default 900 python bench.py --workload trace --steps 3 --warmup 1 --no-cpu ;;
-    dma_split) # the copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent of columns>), 1 MiB per object; needs a measurement build: make -C infinicache_amd/csrc HIPFLAGS+=-DRSGPU_MEASURE_DMA_SPLIT
+    dma_split) # the copy engine beside the zero-copy pass (RSGPU_DMA_SPLIT=<percent of columns>), 1 MiB per object
             RSGPU_DMA_SPLIT=40 run pytest_dma_split 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random.py tests/test_c_abi.py -m gpu -x -q --timeout 150 --timeout-method thread
             for rep in 1 2; do
               for pct in ${DMA_PCTS:-0 20 30 40 50}; do
@@ -116,6 +116,10 @@ PY
     sq)     # issue / wait / clock counters per kernel (one pass per workload; 8 SQ + 2 GRBM slots)
             for wl in ${SQ_WLS:-dec4_get encdec}; do
               run sq_$wl 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT -d gpurun_out/sq_$wl -o run --output-format csv -- python3 bench.py --no-cpu --no-pmc --steps 5 --warmup 50 --workload $wl
+            done ;;
+    tri)    # input-triples kernel vs single inputs (kbench, cold), then the library default through the bench
+            for sh in ${TRI_SHAPES:-decx10_4 decx10_4@1 enc10_4 ver10_4}; do
+              KB_SET=tri KB_ROT=${TRI_ROT:-3} run kbench_tri_${sh/@/_at} 300 ./tools/kbench $sh ${TRI_ROUNDS:-10}
             done ;;
     rehearse8) # the N = 8 scaling harness on the one-GPU box (8 gloo ranks sharing cuda:0), full batch
             BENCH_DIST_BACKEND=gloo BENCH_SHARE_GPU=1 run rehearse8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 ;;

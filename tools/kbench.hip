@@ -760,6 +760,24 @@ std::vector<Variant> twophase_variants() {
     };
 }
 
+// KB_SET=tri: the library's own launch (launch_plan) with the input-triples
+// kernel off / on (set_tri_mode), 16-B and 8-B lanes; the reference output
+// is the single-input kernel's (mode 0)
+template <int K, int R, int MODE>
+void launch_lib_tri(const void *args, dim3 grid, hipStream_t st) {
+    set_tri_mode(MODE);
+    launch_lib<K, R>(args, grid, st);
+    set_tri_mode(0);
+}
+template <int K, int R>
+std::vector<Variant> tri_variants() {
+    return {
+        {"lib, single inputs", launch_lib_tri<K, R, 0>, 1, 256, false},
+        {"lib, gf_apply_tri", launch_lib_tri<K, R, 1>, 1, 256, false},
+        {"xor-only ceiling", launch_x<K, R>, 1, 256, true},
+    };
+}
+
 template <int K, int R>
 std::vector<Variant> stream_variants() {
     return {
@@ -774,6 +792,7 @@ std::vector<Variant> stream_variants() {
 
 template <int K, int R>
 std::vector<Variant> variants() {
+    if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "tri") return tri_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "stream") return stream_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "rows") return rows_variants<K, R>();
     if (std::getenv("KB_SET") && std::string(std::getenv("KB_SET")) == "multi") return multi_variants<K, R>();
@@ -914,7 +933,8 @@ int run(rsgpu_ctx *ctx, Plan &plan, size_t S, int nobj, int rounds, const char *
     auto grid = [&](const Variant &v) {
         return dim3((a.nvec + v.BS * v.U - 1) / (v.BS * v.U), nobj);
     };
-    // reference output from the library's own pass
+    // reference output from the library's own pass (single-input kernel)
+    set_tri_mode(0);
     CK(hipMemset(bad, 0, nobj * 4));
     CK(launch_plan(plan, Layout{d, stride, pitch, S, nobj}, bad, st));
     CK(hipStreamSynchronize(st));

@@ -27,7 +27,8 @@ def short(name: str) -> str:
     if m.group(2) is None:
         return m.group(1)
     args = [a.strip() for a in m.group(2).split(",")]
-    return f"{m.group(1)}<{','.join(args[:2])}>" if m.group(1) == "gf_apply_kernel" else f"{m.group(1)}<{args[0]}>"
+    two = m.group(1) in ("gf_apply_kernel", "gf_apply_tri")  # <K, R, ...>
+    return f"{m.group(1)}<{','.join(args[:2])}>" if two else f"{m.group(1)}<{args[0]}>"
 
 
 def per_kernel(path, counter):
