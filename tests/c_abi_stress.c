@@ -35,6 +35,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "rsgpu.h"
 
@@ -220,5 +221,18 @@ int main(int argc, char **argv) {
     for (int i = 0; i < ROUTES; i++) printf(" %ld", counts[i]);
     printf("), worker served %llu declined %llu launches %llu: %s\n", (unsigned long long)served,
            (unsigned long long)declined, (unsigned long long)launches, bad ? "FAILED" : "all bit-exact");
+    fflush(stdout);
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+    /* every context is destroyed and no worker runs: under ASan the process
+     * ends here, before the HIP runtime's own static destruction, where ASan's
+     * device-allocation tracking aborts when its quarantine recycles a device
+     * chunk after the runtime has unloaded (a CHECK in
+     * sanitizer_allocator_device.h, seen once in round 6 inside libamdhip64's
+     * __cxa_finalize; outside this library).  c_abi_client.c keeps the normal
+     * exit, including the exit with a resident worker. */
+    _exit(bad ? 1 : 0);
+#endif
+#endif
     return bad ? 1 : 0;
 }

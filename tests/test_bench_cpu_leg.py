@@ -66,3 +66,18 @@ def test_cpu_baseline_checked_get_forms():
     assert "Reconstruct then Verify" in cpu["decode_form"]
     assert "bit-exact vs GPU (parity, and the rows the GPU rebuilt from garbage in the work check): True" \
         in cpu["sample"]
+
+
+def test_pass_symbol_follows_the_library_dispatch():
+    """bench.py names the kernel a pass runs as gf_kernels.hip dispatches it:
+    gf_apply_tri for its (K, R, KI) shapes on rows past 128 16-B vectors of an
+    object-major batch, gf_apply_kernel otherwise (the names rocprofv3 and the
+    live PMC passes match on)."""
+    S4 = (4 << 20) // 10 + 1
+    assert bench.pass_symbol(12, 4, 2, S4) == "gf_apply_tri<12,4>"      # dec4_get
+    assert bench.pass_symbol(14, 4, 4, S4) == "gf_apply_tri<14,4>"      # upstream Verify
+    assert bench.pass_symbol(10, 2, 0, 104858) == "gf_apply_kernel<10,2>"  # headline
+    assert bench.pass_symbol(12, 4, 2, 2048) == "gf_apply_kernel<12,4>"   # 128 vectors: small form
+    assert bench.pass_symbol(12, 4, 2, 2049) == "gf_apply_tri<12,4>"
+    assert bench.pass_symbol(12, 4, 2, S4, shard_major=True) == "gf_apply_kernel<12,4>"
+    assert bench.pass_symbol(12, 4, 1, S4) == "gf_apply_kernel<12,4>"     # not an instantiated shape
