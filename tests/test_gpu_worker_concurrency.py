@@ -297,3 +297,32 @@ def test_retired_frees_stay_bounded(gpu):
     st = ia.retired_stats()
     assert st["deferred"] == d1 and st["count"] == 0, st
     enc.worker_stop()
+
+
+def test_user_free_held_is_counted_by_its_size(gpu):
+    """a user's rsgpu_host_free held back while a worker kernel
+    is resident counts toward the kept-bytes bound by the allocation's size
+    (from the library's pin table; the runtime's address-range query does not
+    know every hipHostMalloc'd pointer), so the bound also covers user frees."""
+    import ctypes
+    enc = ia.New(K, P)
+    enc.worker_start(nslots=8, idle_us=1000000)
+    L = ia._lib.load()
+    nbytes = 24 << 20
+    with _Busy(enc) as busy:
+        time.sleep(0.05)  # the callers keep the kernel resident
+        p = ctypes.c_void_p()
+        assert L.rsgpu_host_alloc(nbytes, ctypes.byref(p)) == 0
+        before = ia.retired_stats()
+        assert L.rsgpu_host_free(p) == 0
+        after = ia.retired_stats()
+    assert not busy.errors, busy.errors[:2]
+    assert after["deferred"] == before["deferred"] + 1, (before, after)  # held back: the kernel was resident
+    assert after["bytes"] - before["bytes"] >= nbytes, (before, after)   # ... and counted by its size
+    time.sleep(1.5)  # the kernel leaves after idle_us; the next free lets go of everything
+    q = ctypes.c_void_p()
+    assert L.rsgpu_host_alloc(1 << 16, ctypes.byref(q)) == 0
+    assert L.rsgpu_host_free(q) == 0
+    st = ia.retired_stats()
+    assert st["count"] == 0 and st["bytes"] == 0, st
+    enc.worker_stop()
