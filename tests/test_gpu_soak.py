@@ -25,7 +25,11 @@ than tests/test_gpu_random.py:
     several slabs), and pageable objects of 13-20 MB whose staging copies
     run on the host copy pool;
   * round 5: the host batch pipeline over random arenas (adjacent small
-    objects in one H2D), pinned and pageable, with per-object Get patterns.
+    objects in one H2D), pinned and pageable, with per-object Get patterns;
+  * round 6: device batches of the codes the input-triples kernel serves
+    (gf_apply_tri: RS(10+4) encode, Verify and Gets with 2-3 lost shards,
+    RS(10+3) and RS(12+4) Verify) on rows past 128 vectors, with corrupted
+    extra (checked) shards that must flag exactly their objects.
 Every result is compared bit-exact (bytes) or exactly (booleans, error
 classes) with the oracle on the same input.  Prints a per-kind case count."""
 import collections
@@ -185,6 +189,67 @@ def _device_case(rng, counts):
             assert np.array_equal(a, coded[o, i * pitch:i * pitch + S]), (tag, op, o, i)
     # bytes outside the rebuilt rows' valid ranges are untouched (gaps, pads of other rows)
     assert np.array_equal(out[:, n * pitch:], got[:, n * pitch:]), tag
+
+
+def _tri_case(rng, counts):
+    import torch
+    k, p = [(10, 4), (10, 4), (10, 3), (12, 4)][int(rng.integers(0, 4))]
+    n = k + p
+    S = int(rng.integers(2049, 60000))
+    pitch = (S + 3) // 4 * 4 if rng.random() < 0.3 else (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+    stride = n * pitch + 16 * int(rng.integers(0, 4))
+    nobj = int(rng.integers(1, 12))
+    kind = str(rng.choice(["vandermonde", "cauchy"]))
+    enc = ia.New(k, p, matrix=kind)
+    m = enc.matrix()
+    host = rng.integers(0, 256, (nobj, stride), dtype=np.uint8)
+    for i in range(n):
+        host[:, i * pitch + S:(i + 1) * pitch] = 0
+    buf = torch.from_numpy(host.copy()).cuda()
+    st = torch.cuda.current_stream()
+    tag = ("tri", k, p, S, pitch, stride, nobj, kind)
+    enc.encode_dev(buf, S, pitch, stride, nobj, st)
+    torch.cuda.synchronize()
+    coded = host.copy()
+    oracle.code_batch(m[k:], list(range(k)), list(range(k, n)), coded.reshape(-1), stride, pitch, S, nobj,
+                      nthreads=8)
+    assert np.array_equal(buf.cpu().numpy(), coded), tag
+    counts["tri_encode"] += 1
+    got = coded.copy()
+    if rng.random() < 0.4:  # Verify: every parity row checked
+        hit = sorted(set(rng.integers(0, nobj, int(rng.integers(0, min(nobj, 4) + 1))).tolist()))
+        for o in hit:
+            got[o, int(rng.integers(0, n)) * pitch + int(rng.integers(0, S))] ^= int(rng.integers(1, 256))
+        buf = torch.from_numpy(got).cuda()
+        bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+        enc.verify_dev(buf, S, pitch, stride, nobj, bad, st)
+        torch.cuda.synchronize()
+        assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit, tag
+        counts["tri_verify"] += 1
+        return
+    # a Get: 2 or 3 shards lost (data or parity), the extra present shards checked
+    lost = sorted(rng.choice(n, int(rng.integers(2, min(p, 3) + 1)), replace=False).tolist())
+    present = [i not in lost for i in range(n)]
+    extras = [i for i in range(n) if present[i]][k:]
+    hit = []
+    if extras and rng.random() < 0.6:
+        hit = sorted(set(rng.integers(0, nobj, int(rng.integers(1, min(nobj, 3) + 1))).tolist()))
+        for o in hit:
+            e = extras[int(rng.integers(0, len(extras)))]
+            got[o, e * pitch + int(rng.integers(0, S))] ^= int(rng.integers(1, 256))
+    for o in range(nobj):
+        for i in lost:
+            got[o, i * pitch:i * pitch + S] = rng.integers(0, 256, S, dtype=np.uint8)
+    buf = torch.from_numpy(got.copy()).cuda()
+    bad = torch.full((nobj,), 9, dtype=torch.int32, device="cuda")
+    enc.decode_dev(buf, present, S, pitch, stride, nobj, bad, st)
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    assert np.flatnonzero(bad.cpu().numpy()).tolist() == hit, (tag, lost, hit)
+    for o in range(nobj):  # rebuilt from the first k present, which no corruption touched
+        for i in lost:
+            assert np.array_equal(out[o, i * pitch:i * pitch + S], coded[o, i * pitch:i * pitch + S]), (tag, lost, o, i)
+    counts[f"tri_get_{len(lost)}lost"] += 1
 
 
 def _masks_case(rng, counts):
@@ -615,8 +680,10 @@ def test_gpu_soak_vs_oracle(gpu):
         r = rng.random()
         if r < 0.22:
             _host_case(rng, counts)
-        elif r < 0.42:
+        elif r < 0.36:
             _device_case(rng, counts)
+        elif r < 0.42:
+            _tri_case(rng, counts)
         elif r < 0.54:
             _masks_case(rng, counts)
         elif r < 0.66:
