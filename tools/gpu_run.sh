@@ -121,6 +121,13 @@ PY
             for sh in ${TRI_SHAPES:-decx10_4 decx10_4@1 enc10_4 ver10_4}; do
               KB_SET=tri KB_ROT=${TRI_ROT:-3} run kbench_tri_${sh/@/_at} 300 ./tools/kbench $sh ${TRI_ROUNDS:-10}
             done ;;
+    wsweep) # occupancy cap (RSGPU_MIXED_W workgroups per CU) of the fused RS(10+4) Get, 4 MiB, cold, two passes
+            for rep in 1 2; do
+              for w in ${WS:-3 4 5 6 8}; do
+                RSGPU_MIXED_W=$w KB_LOST=0,5 run wsweep_w${w}_$rep 120 ./tools/kbench lib:dec10_4@4 10
+              done
+            done
+            grep -h "^lib" gpurun_out/wsweep_w*.log > gpurun_out/wsweep_summary.txt || true ;;
     rehearse8) # the N = 8 scaling harness on the one-GPU box (8 gloo ranks sharing cuda:0), full batch
             BENCH_DIST_BACKEND=gloo BENCH_SHARE_GPU=1 run rehearse8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 ;;
     pcie)   run pcie 300 ./tools/pcie_bench ;;
