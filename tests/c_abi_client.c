@@ -161,9 +161,12 @@ static int gpu_checks(void) {
  *   Then a Get whose extra present parity shard is corrupted: Reconstruct
  *   succeeds, the second Verify is false -> decode's error path.  The fused
  *   forms (rsgpu_encode_verify_image, rsgpu_decode_image) give the same
- *   booleans and bytes. */
-static int ecredis_replay(size_t N, int worker) {
-    const int k = 10, p = 2, n = 12;
+ *   booleans and bytes.
+ * p = 2: the client's own RS(10+2).  p = 4: BASELINE config 3's RS(10+4) Get
+ * (data shard 3 and parity 10 lost: 12 of 14 present, 2 extra shards the
+ * second Verify checks; then 13 present with the last shard corrupted). */
+static int ecredis_replay(size_t N, int worker, int p) {
+    const int k = 10, n = k + p;
     const size_t S = (N + k - 1) / k;
     rsgpu_ctx *ctx;
     CHECK(rsgpu_create(k, p, RSGPU_ALL_DEVICES, 0, &ctx) == RSGPU_OK);
@@ -177,8 +180,8 @@ static int ecredis_replay(size_t N, int worker) {
     CHECK(rsgpu_encode_image(ctx, split, S, n) == RSGPU_OK);
     int ok = 0;
     CHECK(rsgpu_verify_image(ctx, split, S, n, &ok) == RSGPU_OK && ok == 1);
-    uint8_t *ref[12];
-    size_t lens[12];
+    uint8_t *ref[16];
+    size_t lens[16];
     for (int i = 0; i < n; i++) {
         ref[i] = malloc(S);
         memcpy(ref[i], split + i * S, S);
@@ -194,17 +197,17 @@ static int ecredis_replay(size_t N, int worker) {
     /* ---- Client.decode (ecRedis.go:404-432): 12 separate Get buffers */
     for (int trial = 0; trial < 2; trial++) {
         const int lost[2] = {3, 10};
-        uint8_t *got[12];
+        uint8_t *got[16];
         for (int i = 0; i < n; i++) {
             got[i] = (i == lost[0] || i == lost[1]) ? NULL : malloc(S);
             lens[i] = got[i] ? S : 0;
             if (got[i]) memcpy(got[i], split + i * S, S);
         }
-        if (trial == 1) {  /* an 11-present Get: shard 10 arrives too; the extra (11) is corrupted */
+        if (trial == 1) {  /* shard 10 arrives too; the last extra shard (n - 1) is corrupted */
             got[10] = malloc(S);
             memcpy(got[10], split + 10 * S, S);
             lens[10] = S;
-            got[11][S / 2] ^= 0x20;
+            got[n - 1][S / 2] ^= 0x20;
         }
         /* stats.AllGood, _ = Verify(data): nil shards -> (false, ErrShardSize) */
         ok = 7;
@@ -244,7 +247,7 @@ static int ecredis_replay(size_t N, int worker) {
         uint64_t pres2 = 0;
         for (int i = 0; i < n; i++)
             if (i != lost[0] && (i != lost[1] || trial == 1)) {
-                memcpy(img2 + i * S, i == 11 && trial == 1 ? got[11] : split + i * S, S);
+                memcpy(img2 + i * S, i == n - 1 && trial == 1 ? got[n - 1] : split + i * S, S);
                 pres2 |= 1ull << i;
             }
         int fused_ok = 7;
@@ -265,8 +268,8 @@ static int ecredis_replay(size_t N, int worker) {
         printf("worker: %llu calls served, %llu launches\n", (unsigned long long)served, (unsigned long long)launches);
     }
     rsgpu_destroy(ctx);
-    printf("ecredis replay ok (%zu-B object%s; Client.encode/decode call order, contiguous and staged routes)\n", N,
-           worker ? ", resident worker" : "");
+    printf("ecredis replay ok (RS(10+%d), %zu-B object%s; Client.encode/decode call order, contiguous and staged "
+           "routes)\n", p, N, worker ? ", resident worker" : "");
     return 0;
 }
 
@@ -304,6 +307,7 @@ int main(int argc, char **argv) {
     if (argc > 1 && strcmp(argv[1], "exit_with_worker") == 0) return exit_with_worker();
     if (host_checks()) return 1;
     if (argc > 1 && strcmp(argv[1], "gpu") == 0)
-        return gpu_checks() || ecredis_replay(1 << 20, 0) || ecredis_replay(1024, 1);
+        return gpu_checks() || ecredis_replay(1 << 20, 0, 2) || ecredis_replay(1024, 1, 2) ||
+               ecredis_replay(4 << 20, 0, 4);
     return 0;
 }

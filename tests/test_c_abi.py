@@ -39,6 +39,8 @@ def test_c_abi_gpu_paths(gpu, client_bin):
     assert r.returncode == 0, r.stderr + r.stdout
     assert "gpu checks ok" in r.stdout
     assert "ecredis replay ok" in r.stdout
+    # BASELINE config 3's Get (RS(10+4), 4 MiB: 12 and 13 of 14 shards present)
+    assert "ecredis replay ok (RS(10+4), 4194304-B object" in r.stdout
 
 
 @pytest.mark.gpu
