@@ -300,13 +300,14 @@ __global__ __launch_bounds__(kBlock) void gf_apply_generic(const GenericArgs a) 
 
 inline unsigned generic_lds(int K, int R) { return (unsigned)((K * R + 1) / 2 * 16 + K / 3 * R * 32); }
 
-// Specialised passes (K <= 16) that are VALU-bound and store rows: the
-// generic kernel's input triples, with K, R and the trailing identity inputs
-// KI known at compile time.  The fused Get of RS(10+4) with 2 extra parity
-// shards (K = 12, R = 4: 2 rows written, 2 checked, KI = 2) issued 1,197
-// VALU instructions per wave with single inputs, at 84 % VALUBusy and a
-// 2.24 GHz held clock against the headline encode's 52 % and 2.40 GHz
-// (profiles/r06_sq_dec4_get.json): the SIMDs' issue, not HBM, set its time.
+// Specialised passes (K <= 16) of the VALU-heavy shapes tri_shape lists
+// (rows written or checked): the generic kernel's input triples, with K, R
+// and the trailing identity inputs KI known at compile time.  The fused Get
+// of RS(10+4) with 2 extra parity shards (K = 12, R = 4: 2 rows written, 2
+// checked, KI = 2) issued 1,197 VALU instructions per wave with single
+// inputs, at 84 % VALUBusy and a 2.24 GHz held clock against the headline
+// encode's 52 % and 2.40 GHz (profiles/r06_sq_dec4_get_single_inputs.json);
+// this kernel issues 976 (r06_sq_dec4_get.json).
 //   * the G = K - KI GF inputs go as NT = G / 3 triples (8 v_perm + 4 xor3
 //     per row and dword for three inputs), the G mod 3 rest as one input or a
 //     pair through the 5-word tables; identity inputs are one XOR each;
