@@ -430,16 +430,13 @@ def under_profiler() -> bool:
         "rocprof" in os.environ.get("LD_PRELOAD", "")
 
 
-def pmc_traffic_live(args, kernel_key, alg_bytes):
-    """HBM bytes per launch of `kernel_key` measured in THIS run: two child
-    runs of this same workload (3 warm-up + 3 timed steps, same batch
-    rotation) under `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
-    (separate passes: the TCC block cannot hold both, MI355X_MICROARCH.md
-    §rocprofv3 PMC slots), each averaged over that kernel's dispatches;
-    read = 2 x FETCH_SIZE (the gfx950 correction of MI355X_MICROARCH.md
-    §HBM), write = WRITE_SIZE, both KiB.  The children are separate processes
-    started after this one's timed region (never an exec), each under a
-    time limit; returns (bytes or None, source note)."""
+def _pmc_child(args, counters, timeout=90):
+    """One rocprofv3 --pmc child run of this same workload (3 warm-up + 3
+    timed steps, same batch rotation, no CPU leg, no nested passes), started
+    after this process's timed region as a separate process (never an exec),
+    its process group killed past `timeout` (a refused counter set hangs past
+    SIGTERM).  Returns (path of its counter CSV copy or None, note); the
+    output directory goes whatever happens to the pass."""
     import glob
     import shutil
     import signal
@@ -448,34 +445,53 @@ def pmc_traffic_live(args, kernel_key, alg_bytes):
     exe = shutil.which("rocprofv3")
     if not exe:
         return None, "rocprofv3 not on PATH"
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from pmc_traffic import per_kernel, short
-    key = short(kernel_key)
     # the children are plain one-process runs: no process group of their own
     child_env = {kk: v for kk, v in os.environ.items() if kk != "BENCH_COLLECTIVES"}
     child_env["BENCH_PMC_CHILD"] = "1"
+    with tempfile.TemporaryDirectory(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp")) as out:
+        cmd = [exe, "--pmc", *counters, "-d", out, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--no-cpu",
+               "--no-pmc", "--steps", "3", "--warmup", "3", "--copies", str(args.copies)]
+        if args.batch:
+            cmd += ["--batch", str(args.batch)]
+        p = subprocess.Popen(cmd, env=child_env, stdout=subprocess.DEVNULL,
+                             stderr=subprocess.DEVNULL, start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return None, f"rocprofv3 --pmc {' '.join(counters)} pass timed out ({timeout} s)"
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if rc != 0 or not files:
+            return None, f"rocprofv3 --pmc {' '.join(counters)} pass failed (rc {rc})"
+        keep = tempfile.NamedTemporaryFile(prefix="bench_pmc_", suffix=".csv", delete=False,
+                                           dir=os.environ.get("TMPDIR", "/tmp"))
+        keep.close()
+        shutil.copyfile(files[0], keep.name)
+        return keep.name, "ok"
+
+
+def pmc_traffic_live(args, kernel_key, alg_bytes):
+    """HBM bytes per launch of `kernel_key` measured in THIS run: two child
+    runs of this same workload under `rocprofv3 --pmc FETCH_SIZE` and `--pmc
+    WRITE_SIZE` (separate passes: the TCC block cannot hold both,
+    MI355X_MICROARCH.md §rocprofv3 PMC slots), each averaged over that
+    kernel's dispatches; read = 2 x FETCH_SIZE (the gfx950 correction of
+    MI355X_MICROARCH.md §HBM), write = WRITE_SIZE, both KiB.  Returns (bytes or
+    None, source note)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import per_kernel, short
+    key = short(kernel_key)
     got = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        # the pass's output directory goes whatever happens to the pass (its
-        # counter CSVs can be large)
-        with tempfile.TemporaryDirectory(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp")) as out:
-            cmd = [exe, "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv", "--",
-                   sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--no-cpu",
-                   "--no-pmc", "--steps", "3", "--warmup", "3", "--copies", str(args.copies)]
-            if args.batch:
-                cmd += ["--batch", str(args.batch)]
-            p = subprocess.Popen(cmd, env=child_env, stdout=subprocess.DEVNULL,
-                                 stderr=subprocess.DEVNULL, start_new_session=True)
-            try:
-                rc = p.wait(timeout=90)
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)  # a refused counter set hangs past SIGTERM
-                p.wait()
-                return None, f"rocprofv3 --pmc {counter} pass timed out (90 s)"
-            files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
-            if rc != 0 or not files:
-                return None, f"rocprofv3 --pmc {counter} pass failed (rc {rc})"
-            val = per_kernel(files[0], counter).get(key)
+        path, note = _pmc_child(args, [counter])
+        if path is None:
+            return None, note
+        try:
+            val = per_kernel(path, counter).get(key)
+        finally:
+            os.unlink(path)
         if not val:
             return None, f"rocprofv3 --pmc {counter}: no dispatch of {key}"
         got[counter] = val
@@ -485,6 +501,48 @@ def pmc_traffic_live(args, kernel_key, alg_bytes):
                           f"workload ({got['FETCH_SIZE'][1]} / {got['WRITE_SIZE'][1]} dispatches of {key}), "
                           f"read 2 x FETCH_SIZE = {int(rd)} B + write {int(wr)} B per launch, "
                           f"{(rd + wr) / alg_bytes:.4f} x algorithmic")
+
+
+SQ_COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY",
+               "SQ_WAIT_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+
+
+def pmc_issue_live(args, kernel_key):
+    """Where the dominant kernel's waves spend their cycles, measured in THIS
+    run: one child run under `rocprofv3 --pmc` with 8 SQ and 2 GRBM counters
+    (one pass: the SQ block holds 8, MI355X_MICROARCH.md §rocprofv3 PMC
+    slots), summarised by tools/pmc_sq.py: VALU instructions per wave,
+    VALUBusy (SQ_ACTIVE_INST_VALU x 4 over every SIMD's cycles), the waves'
+    parked (WAIT_ANY) and issue-stalled (WAIT_INST_ANY) shares of their
+    cycles, and the clock the chip held in the pass (GRBM_GUI_ACTIVE / 8 /
+    dispatch time; a profiled pass runs a few % off the unprofiled clock,
+    §DVFS give-back).  Returns a dict or None and a note."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_sq import per_dispatch, summarise
+    from pmc_traffic import short
+    key = short(kernel_key)
+    path, note = _pmc_child(args, SQ_COUNTERS)
+    if path is None:
+        return None, note
+    try:
+        ds = per_dispatch(path).get(key)
+    finally:
+        os.unlink(path)
+    if not ds:
+        return None, f"SQ pass: no dispatch of {key}"
+    sm = summarise(ds)
+    out = {"kernel": key, "dispatches": sm["dispatches"]}
+    for src, dst in (("valu_insts_per_wave", "valu_insts_per_wave"),
+                     ("valu_active_share_of_simd_cycles", "valu_busy"),
+                     ("wait_any_over_wave_cycles", "wait_any_share"),
+                     ("wait_inst_any_over_wave_cycles", "wait_inst_any_share"),
+                     ("active_inst_any_over_wave_cycles", "issuing_share"),
+                     ("clock_GHz_pass_duration", "clock_GHz_in_pass")):
+        if src in sm:
+            out[dst] = sm[src]
+    out["source"] = ("measured in this run: one rocprofv3 --pmc child pass (" + " ".join(SQ_COUNTERS) +
+                     ") of this workload, tools/pmc_sq.py")
+    return out, "ok"
 
 
 def run_trace(args):
@@ -1174,6 +1232,12 @@ def main():
             traffic_src = f"{traffic_src} (live passes: {note})"
     if traffic_src is None:
         traffic, traffic_src = pmc_traffic(kernel_key, args.workload, dom_bytes)
+    # the dominant kernel's issue / wait / clock counters, same conditions
+    issue = None
+    if world == 1 and not args.no_pmc and not os.environ.get("BENCH_PMC_CHILD") and not under_profiler():
+        issue, note = pmc_issue_live(args, kernel_key)
+        if issue is None:
+            log(f"SQ counters not measured: {note}")
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
@@ -1195,6 +1259,7 @@ def main():
         # achieved / peak of the same kernel on each rank's GPU (rank order);
         # achieved and frac above are rank 0's
         "frac_per_rank": frac_ranks,
+        **({"issue": issue} if issue else {}),
     }
 
     warm = None

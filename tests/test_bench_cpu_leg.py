@@ -81,3 +81,33 @@ def test_pass_symbol_follows_the_library_dispatch():
     assert bench.pass_symbol(12, 4, 2, 2049) == "gf_apply_tri<12,4>"
     assert bench.pass_symbol(12, 4, 2, S4, shard_major=True) == "gf_apply_kernel<12,4>"
     assert bench.pass_symbol(12, 4, 1, S4) == "gf_apply_kernel<12,4>"     # not an instantiated shape
+
+
+def test_pmc_sq_summary_from_a_counter_csv(tmp_path):
+    """tools/pmc_sq.py (bench.py's live SQ pass and the committed r06_sq_*
+    summaries): per-dispatch counters folded per kernel, VALUBusy = VALU
+    quad-cycles x 4 over 1024 SIMDs' cycles, the held clock = GRBM_GUI_ACTIVE
+    / 8 / dispatch time."""
+    import csv
+    import sys
+    sys.path.insert(0, str(bench.ROOT) + "/tools")
+    from pmc_sq import per_dispatch, summarise
+    name = "void rsgpu::gf_apply_tri<12, 4, 2, 4>(rsgpu::TriArgs<12>)"
+    vals = {"SQ_WAVES": 1000, "SQ_WAVE_CYCLES": 4_000_000, "SQ_ACTIVE_INST_ANY": 1_200_000,
+            "SQ_ACTIVE_INST_VALU": 1_024_000, "SQ_WAIT_ANY": 2_000_000, "SQ_WAIT_INST_ANY": 800_000,
+            "SQ_INSTS_VALU": 976_000, "SQ_INSTS_SALU": 90_000, "GRBM_GUI_ACTIVE": 8 * 4000, "GRBM_COUNT": 8 * 4000}
+    f = tmp_path / "run_counter_collection.csv"
+    with open(f, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value", "Start_Timestamp",
+                    "End_Timestamp"])
+        for disp in (1, 2):
+            for c, v in vals.items():
+                w.writerow([disp, name, c, v, 1000, 1000 + 2000])  # 2 us per dispatch
+    d = per_dispatch(str(f))
+    assert list(d) == ["gf_apply_tri<12,4>"] and len(d["gf_apply_tri<12,4>"]) == 2
+    sm = summarise(d["gf_apply_tri<12,4>"])
+    assert sm["valu_insts_per_wave"] == 976.0
+    assert sm["valu_active_share_of_simd_cycles"] == round(4 * 1_024_000 / (1024 * 4000), 4)  # 1.0
+    assert sm["wait_any_over_wave_cycles"] == 0.5
+    assert sm["clock_GHz_pass_duration"] == 2.0  # 4000 cycles / 2000 ns
