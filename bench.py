@@ -430,9 +430,9 @@ def under_profiler() -> bool:
         "rocprof" in os.environ.get("LD_PRELOAD", "")
 
 
-def _pmc_child(args, counters, timeout=90):
-    """One rocprofv3 --pmc child run of this same workload (3 warm-up + 3
-    timed steps, same batch rotation, no CPU leg, no nested passes), started
+def _pmc_child(args, counters, timeout=90, warmup=3):
+    """One rocprofv3 --pmc child run of this same workload (`warmup` warm-up +
+    3 timed steps, same batch rotation, no CPU leg, no nested passes), started
     after this process's timed region as a separate process (never an exec),
     its process group killed past `timeout` (a refused counter set hangs past
     SIGTERM).  Returns (path of its counter CSV copy or None, note); the
@@ -451,7 +451,7 @@ def _pmc_child(args, counters, timeout=90):
     with tempfile.TemporaryDirectory(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp")) as out:
         cmd = [exe, "--pmc", *counters, "-d", out, "-o", "run", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--no-cpu",
-               "--no-pmc", "--steps", "3", "--warmup", "3", "--copies", str(args.copies)]
+               "--no-pmc", "--steps", "3", "--warmup", str(warmup), "--copies", str(args.copies)]
         if args.batch:
             cmd += ["--batch", str(args.batch)]
         p = subprocess.Popen(cmd, env=child_env, stdout=subprocess.DEVNULL,
@@ -521,7 +521,9 @@ def pmc_issue_live(args, kernel_key):
     from pmc_sq import per_dispatch, summarise
     from pmc_traffic import short
     key = short(kernel_key)
-    path, note = _pmc_child(args, SQ_COUNTERS)
+    # 100 warm-up steps: the shader clock ramps over the first ~0.1 s of load;
+    # the summary takes the last dispatches (the child's timed steps)
+    path, note = _pmc_child(args, SQ_COUNTERS, warmup=100)
     if path is None:
         return None, note
     try:
@@ -530,6 +532,7 @@ def pmc_issue_live(args, kernel_key):
         os.unlink(path)
     if not ds:
         return None, f"SQ pass: no dispatch of {key}"
+    ds = ds[-6:]  # 3 timed steps x at most 2 launches of the kernel per step
     sm = summarise(ds)
     out = {"kernel": key, "dispatches": sm["dispatches"]}
     for src, dst in (("valu_insts_per_wave", "valu_insts_per_wave"),
