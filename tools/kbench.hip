@@ -760,6 +760,36 @@ std::vector<Variant> twophase_variants() {
     };
 }
 
+// memory-pattern ceiling under the product's launch policy: the same loads and
+// stores as the pass, XOR instead of GF math, XCD-contiguous workgroup order
+// and the occupancy cap of passes that store and check rows (W = 4
+// workgroups per CU through an LDS reservation), nt loads and stores
+template <int K, int R>
+__global__ __launch_bounds__(256) void xor_policy(const ApplyArgs<K, R> a) {
+    uint32_t obj, chunk;
+    if (!wg_item(a.ord, obj, chunk)) return;
+    const uint32_t v = chunk * 256 + threadIdx.x;
+    if (v >= a.nvec) return;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.base + (uint64_t)obj * a.obj_stride), (short)0, (int)a.p.span, 0x00020000);
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16u, a.p.in_off[c], 2);
+    u32x4 acc = x[0];
+#pragma unroll
+    for (int c = 1; c < K; ++c) acc ^= x[c];
+    for (uint32_t r = 0; r < a.p.nw; ++r)
+        __builtin_amdgcn_raw_buffer_store_b128(acc, rs, v * 16u, a.p.out_off[r], 2);
+    if (a.p.nw == 0 && acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) a.bad[0] = 1;  // keep live
+}
+template <int K, int R, int W>
+void launch_xp(const void *args, dim3 grid, hipStream_t st) {
+    ApplyArgs<K, R> a = *(const ApplyArgs<K, R> *)args;
+    unsigned nb;
+    a.ord = order_for<0>(grid, 0, nb);
+    hipLaunchKernelGGL((xor_policy<K, R>), dim3(nb), dim3(256), W ? (160u * 1024u) / W - 256u : 0u, st, a);
+}
+
 // KB_SET=tri: the library's own launch (launch_plan) with the input-triples
 // kernel off / on (set_tri_mode), 16-B and 8-B lanes; the reference output
 // is the single-input kernel's (mode 0)
@@ -775,6 +805,8 @@ std::vector<Variant> tri_variants() {
         {"lib, single inputs", launch_lib_tri<K, R, 0>, 1, 256, false},
         {"lib, gf_apply_tri", launch_lib_tri<K, R, 1>, 1, 256, false},
         {"xor-only ceiling", launch_x<K, R>, 1, 256, true},
+        {"xor-only, product policy W4", launch_xp<K, R, 4>, 1, 256, true},
+        {"xor-only, XCD order, no cap", launch_xp<K, R, 0>, 1, 256, true},
     };
 }
 
